@@ -1,0 +1,119 @@
+/* kzg_gpu.h -- C ABI of the MI355X KZG engine (libkzgx.so).
+ *
+ * This is the drop-in boundary under the reference's C++ API
+ * (kzg::trusted_setup, /root/reference/src/kzg.h:182-290).  The reference has
+ * no FFI of its own; these entry points replace, one for one:
+ *
+ *   kzgx_msm_g1*            trusted_setup::polyeval_G1  src/trusted_setup.cpp:149-174
+ *                           (private, declared src/kzg.h:187) -- the G1 MSM
+ *                           behind create_commit (:137-142), verify_commit
+ *                           (:144-147), create_proof (:227), verify_proof (:246)
+ *   kzgx_quotient_single*   q = (P - I) / Z for one opening, trusted_setup.cpp:214-225
+ *                           (chunk_length == 1: I = P(z), Z = X - z)
+ *   kzgx_prove_single_batch create_proof(poly, z, 1) for many (poly, z) pairs
+ *   kzgx_poly_eval          evaluate_polynomial_points, src/util.cpp:186-211
+ *   kzgx_poly_interpolate   polyfit / linear_roots_and_polyfit, src/util.cpp:172-184
+ *   kzgx_gen_srs_g1*        trusted_setup(int) G1 part, trusted_setup.cpp:21-74,123-135
+ *   kzgx_load_srs_g1        trusted_setup(const string&) G1 part, trusted_setup.cpp:76-101
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no torch / HIP types in signatures
+ *     (streams are passed as void*, NULL = the context's own stream);
+ *   - scalars / Fr elements: 4 x uint64 little-endian, canonical (< r);
+ *   - G1 points: canonical affine x || y, each coordinate W64 = 4 (BN254) or
+ *     6 (BLS12-381) uint64 little-endian limbs; infinity is x = y = 0 (never
+ *     on either curve since b != 0) and is also flagged in *_is_inf outputs;
+ *   - "_device" entry points take device pointers and enqueue work
+ *     asynchronously on the given stream; the others take host pointers and
+ *     block until the result is on the host;
+ *   - every function returns KZGX_OK (0) or a negative status; kzgx_strerror
+ *     names it.  The C++ facade (include/kzg.h) maps statuses onto the
+ *     reference's exception types.
+ *   - one context per thread (contexts are not internally locked).
+ */
+#ifndef KZG_GPU_H
+#define KZG_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KZGX_OK 0
+#define KZGX_ERR_ARG -1        /* invalid argument (std::invalid_argument) */
+#define KZGX_ERR_HIP -2        /* HIP runtime failure */
+#define KZGX_ERR_OOM -3        /* device allocation failed */
+#define KZGX_ERR_NO_SRS -4     /* no SRS loaded */
+#define KZGX_ERR_DEGREE -5     /* more coefficients than SRS points */
+#define KZGX_ERR_INTERNAL -6
+#define KZGX_ERR_NO_DEVICE -7  /* no usable gfx950 device */
+#define KZGX_ERR_DIV_ZERO -8   /* duplicate interpolation node (NTL: division by zero) */
+
+#define KZGX_CURVE_BN254 0     /* miracl-core BN254 (Nogami), config/curve_BN254 */
+#define KZGX_CURVE_BLS12381 1  /* BLS12-381, config/curve_BLS12381 */
+
+typedef struct kzgx_ctx kzgx_ctx;
+
+const char* kzgx_strerror(int status);
+/* uint64 limbs per base-field coordinate (4 or 6), or -1 */
+int kzgx_base_limbs(int curve);
+
+int kzgx_create(kzgx_ctx** out, int curve, int device);
+void kzgx_destroy(kzgx_ctx* ctx);
+int kzgx_sync(kzgx_ctx* ctx);
+int kzgx_curve(const kzgx_ctx* ctx);
+size_t kzgx_srs_size(const kzgx_ctx* ctx);
+
+/* ---- SRS ---------------------------------------------------------------- */
+/* upload n canonical affine points as the G1 SRS (replaces any previous one) */
+int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n);
+/* generate [tau^(start+i)] G1, i < n, on the GPU and install it as the SRS */
+int kzgx_gen_srs_g1(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n);
+/* copy the installed SRS back (canonical affine) */
+int kzgx_get_srs_g1(kzgx_ctx* ctx, uint64_t* xy, size_t n);
+
+/* ---- MSM (polyeval_G1) ---------------------------------------------------- */
+/* out = sum_{i<n} scalars[i] * SRS[i].  n == 0 gives infinity. */
+int kzgx_msm_g1(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out_xy, int* out_is_inf);
+/* batch of independent MSMs over the same SRS prefix: scalars[b*n + i] */
+int kzgx_msm_g1_batch(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, size_t batch, uint64_t* out_xy,
+                      int* out_is_inf);
+/* device pointers; scalar_stride = distance between consecutive MSMs in
+ * scalars; out_xy: batch x 2 x W64 limbs; out_is_inf: batch x uint32 */
+int kzgx_msm_g1_batch_device(kzgx_ctx* ctx, const void* d_scalars, size_t n, size_t batch, size_t scalar_stride,
+                             void* d_out_xy, void* d_out_is_inf, void* stream);
+
+/* ---- single-opening proofs (create_proof(poly, z, 1)) --------------------- */
+/* q_j = (P_j - P_j(z_j)) / (X - z_j) (n-1 coefficients), y_j = P_j(z_j).
+ * coeff_stride == 0 -> every opening uses the same polynomial. */
+int kzgx_quotient_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
+                                      const void* d_z, size_t batch, void* d_q, size_t q_stride, void* d_y,
+                                      void* stream);
+/* quotient + MSM per opening; host pointers.  out_y may be NULL. */
+int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
+                            const uint64_t* zs, size_t batch, uint64_t* out_xy, int* out_is_inf, uint64_t* out_y);
+/* device pipeline: quotients into the workspace, then one batched MSM */
+int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
+                                   const void* d_z, size_t batch, void* d_out_xy, void* d_out_is_inf, void* d_y,
+                                   void* stream);
+
+/* ---- scalar-field polynomial ops ----------------------------------------- */
+/* ys[j] = P(xs[j]), j < m */
+int kzgx_poly_eval(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t m, uint64_t* ys);
+/* unique interpolant of degree < n through (xs[i], ys[i]); coeffs: n entries */
+int kzgx_poly_interpolate(kzgx_ctx* ctx, const uint64_t* xs, const uint64_t* ys, size_t n, uint64_t* coeffs);
+
+/* Z = prod (X - xs[i]) (build_linear_roots_tree, src/util.cpp:269-284); z_out: n+1 entries */
+int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z_out);
+
+/* ---- G1 helpers ------------------------------------------------------------ */
+/* out = sum of count affine points (is_inf may be NULL); host pointers */
+int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy, int* out_is_inf);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KZG_GPU_H */

@@ -1,0 +1,359 @@
+// C ABI of libkzgx.so (declared in include/kzg_gpu.h).  Thin host layer:
+// argument checks, staging copies for the host-pointer entry points, and
+// dispatch into the HIP kernels of msm.hip / poly.hip / srs.hip.  No compute
+// happens on the host and there is no CPU fallback: without a gfx950 device
+// kzgx_create fails with KZGX_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "kzgx_internal.hpp"
+
+struct kzgx_ctx {
+  kzgx::Ctx c;
+  uint32_t* d_srs_canon = nullptr;  // installed SRS, canonical affine
+  size_t srs_canon_b = 0;
+};
+
+namespace kzgx {
+
+int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? KZGX_ERR_OOM : KZGX_ERR_HIP; }
+
+int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap) {
+  (void)ctx;
+  if (bytes == 0) bytes = 16;
+  if (*p && bytes <= *cap) return KZGX_OK;
+  if (*p) {
+    KZGX_TRY_HIP(hipDeviceSynchronize());
+    KZGX_TRY_HIP(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+  }
+  // round up to limit re-allocation churn
+  size_t want = bytes + bytes / 8;
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+      *p = nullptr;
+      return hip_fail(e);
+    }
+    want = bytes;
+  }
+  *cap = want;
+  return KZGX_OK;
+}
+
+}  // namespace kzgx
+
+using kzgx::Ctx;
+
+namespace {
+
+int activate(kzgx_ctx* ctx) {
+  if (!ctx) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipSetDevice(ctx->c.device));
+  return KZGX_OK;
+}
+
+hipStream_t pick(kzgx_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->c.stream; }
+
+int stage(kzgx_ctx* ctx, int slot, size_t bytes, void** out) {
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, &ctx->c.d_stage[slot], bytes, &ctx->c.stage_b[slot]));
+  *out = ctx->c.d_stage[slot];
+  return KZGX_OK;
+}
+
+size_t point_words(const kzgx_ctx* ctx) { return 2 * (size_t)ctx->c.base_words(); }
+
+}  // namespace
+
+extern "C" {
+
+const char* kzgx_strerror(int s) {
+  switch (s) {
+    case KZGX_OK: return "ok";
+    case KZGX_ERR_ARG: return "invalid argument";
+    case KZGX_ERR_HIP: return "HIP runtime error";
+    case KZGX_ERR_OOM: return "device out of memory";
+    case KZGX_ERR_NO_SRS: return "no SRS loaded";
+    case KZGX_ERR_DEGREE: return "polynomial degree be at most one less than the setup size (num_coeffs)";
+    case KZGX_ERR_INTERNAL: return "internal error";
+    case KZGX_ERR_NO_DEVICE: return "no gfx950 (MI355X) device available";
+    case KZGX_ERR_DIV_ZERO: return "division by zero (duplicate interpolation point)";
+    default: return "unknown status";
+  }
+}
+
+int kzgx_base_limbs(int curve) {
+  return curve == KZGX_CURVE_BN254 ? 4 : curve == KZGX_CURVE_BLS12381 ? 6 : -1;
+}
+
+int kzgx_create(kzgx_ctx** out, int curve, int device) {
+  if (!out || (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381)) return KZGX_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KZGX_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return KZGX_ERR_ARG;
+  hipDeviceProp_t prop;
+  KZGX_TRY_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return KZGX_ERR_NO_DEVICE;
+  kzgx_ctx* ctx = new (std::nothrow) kzgx_ctx();
+  if (!ctx) return KZGX_ERR_OOM;
+  ctx->c.curve = curve;
+  ctx->c.device = device;
+  ctx->c.W = (257 + ctx->c.c - 1) / ctx->c.c;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return kzgx::hip_fail(e);
+  }
+  *out = ctx;
+  return KZGX_OK;
+}
+
+void kzgx_destroy(kzgx_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->c.device);
+  (void)hipStreamSynchronize(ctx->c.stream);
+  Ctx& c = ctx->c;
+  void* bufs[] = {c.d_table, c.d_inf, c.ws.counts, c.ws.offsets, c.ws.cursors, c.ws.entries, c.ws.bsum,
+                  c.ws.heads, c.ws.tails, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
+                  c.d_poly_ws, ctx->d_srs_canon};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(c.stream);
+  delete ctx;
+}
+
+int kzgx_sync(kzgx_ctx* ctx) {
+  KZGX_TRY(activate(ctx));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_curve(const kzgx_ctx* ctx) { return ctx ? ctx->c.curve : -1; }
+
+size_t kzgx_srs_size(const kzgx_ctx* ctx) { return ctx ? ctx->c.n_srs : 0; }
+
+int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!xy || n == 0) return KZGX_ERR_ARG;
+  const size_t bytes = n * point_words(ctx) * 4;
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs_canon, bytes, &ctx->srs_canon_b));
+  KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_srs_canon, xy, bytes, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::srs_upload(&ctx->c, ctx->d_srs_canon, n));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_gen_srs_g1(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!tau || n == 0 || n > 0x7fffffffu) return KZGX_ERR_ARG;
+  const size_t bytes = n * point_words(ctx) * 4;
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs_canon, bytes, &ctx->srs_canon_b));
+  void* d_tau;
+  KZGX_TRY(stage(ctx, 0, 32, &d_tau));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_tau, tau, 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::gen_srs_points(&ctx->c, (const uint32_t*)d_tau, start, n, ctx->d_srs_canon, ctx->c.stream));
+  KZGX_TRY(kzgx::srs_upload(&ctx->c, ctx->d_srs_canon, n));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_get_srs_g1(kzgx_ctx* ctx, uint64_t* xy, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!xy) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->c.n_srs) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipMemcpyAsync(xy, ctx->d_srs_canon, n * point_words(ctx) * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_msm_g1_batch_device(kzgx_ctx* ctx, const void* d_scalars, size_t n, size_t batch, size_t scalar_stride,
+                             void* d_out_xy, void* d_out_is_inf, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (!d_out_xy || !d_out_is_inf || (n > 0 && !d_scalars) || batch > 65535) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  if (batch > 1 && scalar_stride < n) return KZGX_ERR_ARG;
+  hipStream_t st = pick(ctx, stream);
+  if (n == 0) {  // zero polynomial: ECP_inf (trusted_setup.cpp:150-154)
+    KZGX_TRY_HIP(hipMemsetAsync(d_out_xy, 0, batch * point_words(ctx) * 4, st));
+    std::vector<uint32_t> ones(batch, 1u);
+    KZGX_TRY_HIP(hipMemcpyAsync(d_out_is_inf, ones.data(), batch * 4, hipMemcpyHostToDevice, st));
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+    return KZGX_OK;
+  }
+  return kzgx::msm_batch(&ctx->c, (const uint32_t*)d_scalars, n, batch, scalar_stride * 8, (uint32_t*)d_out_xy,
+                         (uint32_t*)d_out_is_inf, st);
+}
+
+int kzgx_msm_g1_batch(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, size_t batch, uint64_t* out_xy,
+                      int* out_is_inf) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (!out_xy || !out_is_inf || (n > 0 && !scalars)) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  void *d_s = nullptr, *d_o, *d_i;
+  const size_t sb = n * batch * 32, ob = batch * point_words(ctx) * 4;
+  if (n) KZGX_TRY(stage(ctx, 0, sb, &d_s));
+  KZGX_TRY(stage(ctx, 1, ob, &d_o));
+  KZGX_TRY(stage(ctx, 2, batch * 4, &d_i));
+  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx_msm_g1_batch_device(ctx, d_s, n, batch, n, d_o, d_i, nullptr));
+  std::vector<uint32_t> inf(batch);
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, ob, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(inf.data(), d_i, batch * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  for (size_t b = 0; b < batch; b++) out_is_inf[b] = (int)inf[b];
+  return KZGX_OK;
+}
+
+int kzgx_msm_g1(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out_xy, int* out_is_inf) {
+  return kzgx_msm_g1_batch(ctx, scalars, n, 1, out_xy, out_is_inf);
+}
+
+int kzgx_quotient_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
+                                      const void* d_z, size_t batch, void* d_q, size_t q_stride, void* d_y,
+                                      void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (!d_z || (n > 0 && !d_coeffs) || (n > 1 && !d_q) || n > 0xffffffffu) return KZGX_ERR_ARG;
+  if (batch > 1 && coeff_stride != 0 && coeff_stride < n) return KZGX_ERR_ARG;
+  return kzgx::quotient_single(&ctx->c, (const uint32_t*)d_coeffs, n, coeff_stride * 8, (const uint32_t*)d_z, batch,
+                               (uint32_t*)d_q, q_stride * 8, (uint32_t*)d_y, pick(ctx, stream));
+}
+
+int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
+                                   const void* d_z, size_t batch, void* d_out_xy, void* d_out_is_inf, void* d_y,
+                                   void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  const size_t nq = n > 0 ? n - 1 : 0;
+  if (nq > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  hipStream_t st = pick(ctx, stream);
+  void* d_q = nullptr;
+  if (nq) KZGX_TRY(stage(ctx, 3, nq * batch * 32, &d_q));
+  KZGX_TRY(kzgx_quotient_single_batch_device(ctx, d_coeffs, n, coeff_stride, d_z, batch, d_q, nq, d_y, st));
+  return kzgx_msm_g1_batch_device(ctx, d_q, nq, batch, nq, d_out_xy, d_out_is_inf, st);
+}
+
+int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
+                            const uint64_t* zs, size_t batch, uint64_t* out_xy, int* out_is_inf, uint64_t* out_y) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (!zs || !out_xy || !out_is_inf || (n > 0 && !coeffs)) return KZGX_ERR_ARG;
+  if (batch > 1 && coeff_stride != 0 && coeff_stride < n) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  const size_t npolys = coeff_stride == 0 ? 1 : batch;
+  const size_t cb = (npolys - 1) * coeff_stride * 32 + n * 32;
+  const size_t ob = batch * point_words(ctx) * 4;
+  void *d_c = nullptr, *d_z, *d_o, *d_i, *d_y;
+  if (n) KZGX_TRY(stage(ctx, 0, cb, &d_c));
+  KZGX_TRY(stage(ctx, 1, ob + batch * 4, &d_o));
+  d_i = (char*)d_o + ob;
+  KZGX_TRY(stage(ctx, 2, batch * 64, &d_z));
+  d_y = (char*)d_z + batch * 32;
+  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, cb, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_z, zs, batch * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx_prove_single_batch_device(ctx, d_c, n, coeff_stride, d_z, batch, d_o, d_i, d_y, nullptr));
+  std::vector<uint32_t> inf(batch);
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, ob, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(inf.data(), d_i, batch * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  if (out_y) KZGX_TRY_HIP(hipMemcpyAsync(out_y, d_y, batch * 32, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  for (size_t b = 0; b < batch; b++) out_is_inf[b] = (int)inf[b];
+  return KZGX_OK;
+}
+
+int kzgx_poly_eval(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t m, uint64_t* ys) {
+  KZGX_TRY(activate(ctx));
+  if (m == 0) return KZGX_OK;
+  if (!xs || !ys || (n > 0 && !coeffs) || n > 0xffffffffu || m > 0xffffffffu) return KZGX_ERR_ARG;
+  void *d_c = nullptr, *d_x, *d_y;
+  if (n) KZGX_TRY(stage(ctx, 0, n * 32, &d_c));
+  KZGX_TRY(stage(ctx, 1, m * 32, &d_x));
+  KZGX_TRY(stage(ctx, 2, m * 32, &d_y));
+  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xs, m * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::poly_eval(&ctx->c, (const uint32_t*)d_c, n, (const uint32_t*)d_x, m, (uint32_t*)d_y, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(ys, d_y, m * 32, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_poly_interpolate(kzgx_ctx* ctx, const uint64_t* xs, const uint64_t* ys, size_t n, uint64_t* coeffs) {
+  KZGX_TRY(activate(ctx));
+  if (n == 0) return KZGX_OK;
+  if (!xs || !ys || !coeffs || n > (1u << 24)) return KZGX_ERR_ARG;
+  void *d_x, *d_y, *d_c;
+  KZGX_TRY(stage(ctx, 0, n * 32, &d_x));
+  KZGX_TRY(stage(ctx, 1, n * 32, &d_y));
+  KZGX_TRY(stage(ctx, 2, n * 32, &d_c));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xs, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_y, ys, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  int rc = kzgx::poly_interpolate(&ctx->c, (const uint32_t*)d_x, (const uint32_t*)d_y, n, (uint32_t*)d_c,
+                                  ctx->c.stream);
+  if (rc != KZGX_OK) return rc;
+  KZGX_TRY_HIP(hipMemcpyAsync(coeffs, d_c, n * 32, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z_out) {
+  KZGX_TRY(activate(ctx));
+  if (!z_out) return KZGX_ERR_ARG;
+  if (n == 0) {  // empty product = 1
+    std::memset(z_out, 0, 32);
+    z_out[0] = 1;
+    return KZGX_OK;
+  }
+  if (!xs || n > (1u << 24)) return KZGX_ERR_ARG;
+  void *d_x, *d_z;
+  KZGX_TRY(stage(ctx, 0, n * 32, &d_x));
+  KZGX_TRY(stage(ctx, 1, (n + 1) * 32, &d_z));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xs, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::poly_vanishing(&ctx->c, (const uint32_t*)d_x, n, (uint32_t*)d_z, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(z_out, d_z, (n + 1) * 32, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy,
+                int* out_is_inf) {
+  KZGX_TRY(activate(ctx));
+  if (!out_xy || !out_is_inf || (count > 0 && !xy)) return KZGX_ERR_ARG;
+  const size_t pb = point_words(ctx) * 4;
+  void *d_p, *d_f, *d_o;
+  KZGX_TRY(stage(ctx, 0, count * pb + 16, &d_p));
+  KZGX_TRY(stage(ctx, 1, count * 4 + 16, &d_f));
+  KZGX_TRY(stage(ctx, 2, pb + 16, &d_o));
+  std::vector<uint32_t> f(count);
+  for (size_t i = 0; i < count; i++) f[i] = is_inf ? (uint32_t)(is_inf[i] != 0) : 0u;
+  if (count) {
+    KZGX_TRY_HIP(hipMemcpyAsync(d_p, xy, count * pb, hipMemcpyHostToDevice, ctx->c.stream));
+    KZGX_TRY_HIP(hipMemcpyAsync(d_f, f.data(), count * 4, hipMemcpyHostToDevice, ctx->c.stream));
+  }
+  uint32_t* d_oi = (uint32_t*)((char*)d_o + pb);
+  KZGX_TRY(kzgx::g1_sum(&ctx->c, (const uint32_t*)d_p, (const uint32_t*)d_f, count, (uint32_t*)d_o, d_oi,
+                        ctx->c.stream));
+  uint32_t oi = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, pb, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  *out_is_inf = (int)oi;
+  return KZGX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// Internal (host-side) declarations shared by the libkzgx translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/kzg_gpu.h"
+
+#ifndef KZGX_WINDOW_BITS
+#define KZGX_WINDOW_BITS 10
+#endif
+
+#define KZGX_TRY(expr)                 \
+  do {                                 \
+    int _rc = (expr);                  \
+    if (_rc != KZGX_OK) return _rc;    \
+  } while (0)
+
+#define KZGX_TRY_HIP(expr)                              \
+  do {                                                  \
+    hipError_t _e = (expr);                             \
+    if (_e != hipSuccess) return ::kzgx::hip_fail(_e);  \
+  } while (0)
+
+namespace kzgx {
+
+int hip_fail(hipError_t e);
+
+struct MsmWs {
+  uint32_t *counts = nullptr, *offsets = nullptr, *cursors = nullptr, *entries = nullptr;
+  uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr;
+  size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0;
+};
+
+struct Ctx {
+  int curve = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int c = KZGX_WINDOW_BITS;  // window bits
+  int W = 0;                 // windows
+  uint32_t seg_k = 32;       // entries per accumulation thread
+  size_t n_srs = 0;
+  uint32_t* d_table = nullptr;  // [W][n_srs] affine Montgomery points
+  size_t table_bytes = 0;
+  uint8_t* d_inf = nullptr;  // [n_srs]
+  size_t inf_bytes = 0;
+  MsmWs ws;
+  void* d_poly_ws = nullptr;  // scratch for the Fr polynomial kernels
+  size_t poly_ws_b = 0;
+  // staging for host-pointer entry points
+  void* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t stage_b[4] = {0, 0, 0, 0};
+  int base_words() const { return curve == KZGX_CURVE_BN254 ? 8 : 12; }
+};
+
+// grow-only device allocation (frees the old block)
+int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap);
+
+int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
+int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+              uint32_t* d_out_inf, hipStream_t st);
+int gen_srs_points(Ctx* ctx, const uint32_t* tau_canon_host, size_t start, size_t n, uint32_t* d_out_canon,
+                   hipStream_t st);
+int g1_sum(Ctx* ctx, const uint32_t* d_xy, const uint32_t* d_inf, size_t count, uint32_t* d_out, uint32_t* d_out_inf,
+           hipStream_t st);
+
+// scalar field (Fr) kernels, poly.hip
+int quotient_single(Ctx* ctx, const uint32_t* d_coeffs, size_t n, size_t coeff_stride_words, const uint32_t* d_z,
+                    size_t batch, uint32_t* d_q, size_t q_stride_words, uint32_t* d_y, hipStream_t st);
+int poly_eval(Ctx* ctx, const uint32_t* d_coeffs, size_t n, const uint32_t* d_x, size_t m, uint32_t* d_y,
+              hipStream_t st);
+int poly_vanishing(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipStream_t st);
+int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
+                     hipStream_t st);
+
+}  // namespace kzgx

@@ -1,0 +1,404 @@
+// Batched Pippenger G1 MSM for gfx950 -- the hot path behind
+// kzg::trusted_setup::create_commit / create_proof / verify_commit
+// (reference: trusted_setup::polyeval_G1, src/trusted_setup.cpp:149-174,
+// a naive per-term PAIR_G1mul + ECP_add loop).
+//
+// Design (MI355X-first):
+//  * fixed-base windows: at SRS load every point P_i is expanded into W
+//    window copies T[w][i] = 2^(c w) P_i (affine, Montgomery, HBM resident),
+//    so all windows of an MSM share ONE set of 2^(c-1) signed-digit buckets and
+//    there is no per-window doubling chain;
+//  * per MSM b: signed c-bit digits -> (point, sign) entries counting-sorted by
+//    bucket (LDS histograms + one global atomic per (workgroup, bucket));
+//  * bucket accumulation is load balanced: every thread owns exactly K
+//    consecutive sorted entries and does K mixed XYZZ additions; runs that
+//    cross a segment boundary leave head/tail partials that the reduction
+//    kernel merges;
+//  * the reduction (one workgroup per MSM) finishes the buckets, forms
+//    sum (k+1) B_k with an LDS suffix scan + tree, and converts to affine.
+// Every step is an exact group operation, so the affine output is bit-exact
+// with any other correct evaluation of sum c_i [tau^i]G1.
+#include <hip/hip_runtime.h>
+
+#include "curve.hpp"
+#include "kzgx_internal.hpp"
+
+namespace kzgx {
+
+// --------------------------------------------------------------------------
+// SRS upload / fixed-base table
+// --------------------------------------------------------------------------
+// canonical affine (x||y, 2N words per point) -> Montgomery into T[0];
+// all-zero input marks infinity.
+template <class C>
+__global__ void k_srs_to_mont(const uint32_t* __restrict__ canon, uint32_t* __restrict__ table, uint8_t* __restrict__ inf,
+                              uint32_t n) {
+  using F = typename C::Fp;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<C> a = affine_load<C>(canon + (size_t)i * 2 * F::N);
+  bool is_inf = fe_is_zero<F>(a.x) && fe_is_zero<F>(a.y);
+  inf[i] = is_inf ? 1 : 0;
+  a.x = fe_to_mont<F>(a.x);
+  a.y = fe_to_mont<F>(a.y);
+  affine_store<C>(table + (size_t)i * 2 * F::N, a);
+}
+
+// T[w][i] = 2^c T[w-1][i] for w = 1..W-1
+template <class C>
+__global__ void k_table_build(uint32_t* __restrict__ table, const uint8_t* __restrict__ inf, uint32_t n, int W, int c) {
+  using F = typename C::Fp;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t PW = 2 * F::N;
+  Affine<C> a = affine_load<C>(table + (size_t)i * PW);
+  const bool is_inf = inf[i] != 0;
+  for (int w = 1; w < W; w++) {
+    if (!is_inf) {
+      Xyzz<C> p = xyzz_from_affine<C>(a);
+      for (int s = 0; s < c; s++) p = xyzz_dbl<C>(p);
+      if (!xyzz_to_affine<C>(p, a)) {
+        a.x = fe_zero<F>();
+        a.y = fe_zero<F>();
+      }
+    }
+    affine_store<C>(table + ((size_t)w * n + i) * PW, a);
+  }
+}
+
+// --------------------------------------------------------------------------
+// signed-digit recoding
+// --------------------------------------------------------------------------
+template <int CB>
+struct Win {
+  static constexpr int W = (257 + CB - 1) / CB;  // covers any 256-bit integer
+  static constexpr uint32_t NB = 1u << (CB - 1);
+};
+
+// digit w of the scalar (8 canonical LE words); returns signed digit, updates carry
+template <int CB>
+KZGX_DEV int digit_at(const uint32_t (&s)[8], int w, uint32_t& carry) {
+  const int bit = CB * w;
+  const int word = bit >> 5;
+  const int sh = bit & 31;
+  uint32_t raw = 0;
+  if (word < 8) {
+    raw = s[word] >> sh;
+    if (sh + CB > 32 && word + 1 < 8) raw |= s[word + 1] << (32 - sh);
+  }
+  raw &= (1u << CB) - 1u;
+  raw += carry;
+  if (raw > Win<CB>::NB) {
+    carry = 1;
+    return (int)raw - (1 << CB);
+  }
+  carry = 0;
+  return (int)raw;
+}
+
+KZGX_DEV void load_scalar(const uint32_t* p, uint32_t (&s)[8]) {
+  uint4 a = reinterpret_cast<const uint4*>(p)[0];
+  uint4 b = reinterpret_cast<const uint4*>(p)[1];
+  s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+  s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+}
+
+// pass 1: per-MSM bucket histogram
+template <int CB>
+__global__ __launch_bounds__(256) void k_msm_count(const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words,
+                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ counts) {
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  __shared__ uint32_t hist[NB];
+  const uint32_t b = blockIdx.y;
+  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !inf[i]) {
+    uint32_t s[8];
+    load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      int d = digit_at<CB>(s, w, carry);
+      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) {
+    uint32_t h = hist[k];
+    if (h) atomicAdd(&counts[(size_t)b * NB + k], h);
+  }
+}
+
+// pass 2: exclusive scan of the histogram -> offsets[b][0..NB], cursors
+__global__ __launch_bounds__(256) void k_msm_scan(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
+                                                  uint32_t* __restrict__ cursors, uint32_t nb) {
+  __shared__ uint32_t part[256];
+  const uint32_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = nb / 256;  // nb is a multiple of 256
+  const uint32_t* cnt = counts + (size_t)b * nb;
+  uint32_t local = 0;
+  for (uint32_t j = 0; j < per; j++) local += cnt[t * per + j];
+  part[t] = local;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    uint32_t v = (t >= d) ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - local;  // exclusive prefix
+  uint32_t* off = offsets + (size_t)b * (nb + 1);
+  uint32_t* cur = cursors + (size_t)b * nb;
+  for (uint32_t j = 0; j < per; j++) {
+    off[t * per + j] = run;
+    cur[t * per + j] = run;
+    run += cnt[t * per + j];
+  }
+  if (t == 255) off[nb] = run;
+}
+
+// pass 3: scatter (table index | sign) entries into bucket order
+template <int CB>
+__global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                     size_t stride_words, const uint8_t* __restrict__ inf,
+                                                     uint32_t* __restrict__ cursors, uint32_t* __restrict__ entries,
+                                                     size_t emax, uint32_t n_srs) {
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  __shared__ uint32_t lcount[NB];
+  __shared__ uint32_t lbase[NB];
+  const uint32_t b = blockIdx.y;
+  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) lcount[k] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  int dig[W];
+  uint32_t rank[W];
+  const bool live = i < n && !inf[i];
+  if (live) {
+    uint32_t s[8];
+    load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      int d = digit_at<CB>(s, w, carry);
+      dig[w] = d;
+      rank[w] = d != 0 ? atomicAdd(&lcount[(d < 0 ? -d : d) - 1], 1u) : 0u;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) {
+    uint32_t h = lcount[k];
+    lbase[k] = h ? atomicAdd(&cursors[(size_t)b * NB + k], h) : 0u;
+  }
+  __syncthreads();
+  if (live) {
+    uint32_t* out = entries + b * emax;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      int d = dig[w];
+      if (d != 0) {
+        uint32_t k = (uint32_t)((d < 0 ? -d : d) - 1);
+        out[lbase[k] + rank[w]] = ((uint32_t)w * n_srs + i) | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
+// pass 4: balanced bucket accumulation, K entries per thread
+template <class C>
+__global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ entries, size_t emax,
+                                                   const uint32_t* __restrict__ offsets, uint32_t nb,
+                                                   const uint32_t* __restrict__ table, uint32_t K, size_t smax,
+                                                   uint32_t* __restrict__ bsum, uint32_t* __restrict__ heads,
+                                                   uint32_t* __restrict__ tails) {
+  using F = typename C::Fp;
+  constexpr int PW = 2 * F::N;
+  constexpr int XW = 4 * F::N;
+  const uint32_t b = blockIdx.y;
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t* off = offsets + (size_t)b * (nb + 1);
+  const uint32_t E = off[nb];
+  const uint32_t start = seg * K;
+  if (start >= E) return;
+  const uint32_t end = min(start + K, E);
+  // bucket k with off[k] <= start < off[k+1]
+  uint32_t lo = 0, hi = nb;  // invariant off[lo] <= start < off[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= start)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint32_t k = lo;
+  uint32_t next = off[k + 1];
+  bool before = off[k] < start;
+  const uint32_t* ent = entries + b * emax;
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t p = start; p < end; ++p) {
+    if (p == next) {
+      // bucket k ended inside this segment
+      uint32_t* dst = before ? heads + ((size_t)b * smax + seg) * XW : bsum + ((size_t)b * nb + k) * XW;
+      xyzz_store<C>(dst, acc);
+      acc = xyzz_inf<C>();
+      before = false;
+      do {
+        k++;
+        next = off[k + 1];
+      } while (next == p);
+    }
+    const uint32_t e = ent[p];
+    Affine<C> a = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+    if (e >> 31) a.y = fe_neg<F>(a.y);
+    acc = xyzz_add_affine_impl<C>(acc, a);
+  }
+  uint32_t* dst;
+  if (before)
+    dst = heads + ((size_t)b * smax + seg) * XW;
+  else if (next > end)
+    dst = tails + ((size_t)b * smax + seg) * XW;
+  else
+    dst = bsum + ((size_t)b * nb + k) * XW;
+  xyzz_store<C>(dst, acc);
+}
+
+// pass 5: finish buckets, sum_k (k+1) B_k, affine, canonical output
+template <class C>
+__global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
+                                                    size_t smax, const uint32_t* __restrict__ bsum,
+                                                    const uint32_t* __restrict__ heads,
+                                                    const uint32_t* __restrict__ tails, uint32_t* __restrict__ out,
+                                                    uint32_t* __restrict__ out_inf) {
+  using F = typename C::Fp;
+  constexpr int XW = 4 * F::N;
+  extern __shared__ uint32_t lds[];  // 256 points, XW words each
+  const uint32_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t J = nb / 256;
+  const uint32_t* off = offsets + (size_t)b * (nb + 1);
+  Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
+  for (int j = (int)J - 1; j >= 0; j--) {
+    const uint32_t k = t * J + (uint32_t)j;
+    const uint32_t o0 = off[k], o1 = off[k + 1];
+    Xyzz<C> bk = xyzz_inf<C>();
+    if (o1 > o0) {
+      const uint32_t s0 = o0 / K, s1 = (o1 - 1) / K;
+      if (s0 == s1) {
+        bk = xyzz_load<C>(bsum + ((size_t)b * nb + k) * XW);
+      } else {
+        bk = xyzz_load<C>(tails + ((size_t)b * smax + s0) * XW);
+        for (uint32_t s = s0 + 1; s <= s1; s++) bk = xyzz_add<C>(bk, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
+      }
+    }
+    run = xyzz_add<C>(run, bk);
+    sum = xyzz_add<C>(sum, run);
+  }
+  // suffix scan of run totals: S_t = sum_{u >= t} T_u
+  Xyzz<C> S = run;
+  xyzz_store<C>(lds + t * XW, S);
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    Xyzz<C> o = xyzz_inf<C>();
+    if (t + d < 256) o = xyzz_load<C>(lds + (t + d) * XW);
+    __syncthreads();
+    S = xyzz_add<C>(S, o);
+    xyzz_store<C>(lds + t * XW, S);
+    __syncthreads();
+  }
+  // V_t = R_t + J * S_t (t >= 1)
+  if (t >= 1) {
+    for (uint32_t m = J; m > 1; m >>= 1) S = xyzz_dbl<C>(S);
+    sum = xyzz_add<C>(sum, S);
+  }
+  xyzz_store<C>(lds + t * XW, sum);
+  __syncthreads();
+  for (uint32_t h = 128; h >= 1; h >>= 1) {
+    if (t < h) {
+      Xyzz<C> o = xyzz_load<C>(lds + (t + h) * XW);
+      sum = xyzz_add<C>(sum, o);
+      xyzz_store<C>(lds + t * XW, sum);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    Affine<C> a;
+    bool fin = xyzz_to_affine<C>(sum, a);
+    if (fin) {
+      a.x = fe_from_mont<F>(a.x);
+      a.y = fe_from_mont<F>(a.y);
+    }
+    affine_store<C>(out + (size_t)b * 2 * F::N, a);
+    out_inf[b] = fin ? 0u : 1u;
+  }
+}
+
+// --------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------
+template <class C>
+int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
+  using F = typename C::Fp;
+  const int W = ctx->W;
+  const size_t pw = 2 * F::N * sizeof(uint32_t);
+  KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table, (size_t)W * n * pw, &ctx->table_bytes));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_inf, n, &ctx->inf_bytes));
+  dim3 blk(256), grd((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(k_srs_to_mont<C>, grd, blk, 0, ctx->stream, d_canon, ctx->d_table, ctx->d_inf, (uint32_t)n);
+  hipLaunchKernelGGL(k_table_build<C>, grd, blk, 0, ctx->stream, ctx->d_table, ctx->d_inf, (uint32_t)n, W, ctx->c);
+  KZGX_TRY_HIP(hipGetLastError());
+  ctx->n_srs = n;
+  return KZGX_OK;
+}
+
+template <class C, int CB>
+int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+                   uint32_t* d_out_inf, hipStream_t st) {
+  using F = typename C::Fp;
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  const uint32_t K = ctx->seg_k;
+  const size_t emax = (size_t)n * W;
+  const size_t smax = (emax + K - 1) / K;
+  const size_t XB = 4 * F::N * sizeof(uint32_t);
+  MsmWs& ws = ctx->ws;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, batch * NB * 4, &ws.counts_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, batch * (NB + 1) * 4, &ws.offsets_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, batch * NB * 4, &ws.cursors_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.entries, batch * emax * 4, &ws.entries_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, batch * NB * XB, &ws.bsum_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, batch * smax * XB, &ws.heads_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, batch * smax * XB, &ws.tails_b));
+  KZGX_TRY_HIP(hipMemsetAsync(ws.counts, 0, batch * NB * 4, st));
+  dim3 blk(256);
+  dim3 gs((unsigned)((n + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts);
+  hipLaunchKernelGGL(k_msm_scan, dim3((unsigned)batch), blk, 0, st, ws.counts, ws.offsets, ws.cursors, NB);
+  hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.cursors,
+                     ws.entries, emax, (uint32_t)ctx->n_srs);
+  dim3 ga((unsigned)((smax + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL(k_msm_accum<C>, ga, blk, 0, st, ws.entries, emax, ws.offsets, NB, ctx->d_table, K, smax, ws.bsum,
+                     ws.heads, ws.tails);
+  hipLaunchKernelGGL(k_msm_reduce<C>, dim3((unsigned)batch), blk, 256 * XB, st, ws.offsets, NB, K, smax, ws.bsum,
+                     ws.heads, ws.tails, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
+  return ctx->curve == KZGX_CURVE_BN254 ? srs_upload_impl<BN254G1>(ctx, d_canon, n)
+                                        : srs_upload_impl<BLS12381G1>(ctx, d_canon, n);
+}
+
+int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+              uint32_t* d_out_inf, hipStream_t st) {
+  if (ctx->c != KZGX_WINDOW_BITS) return KZGX_ERR_INTERNAL;
+  return ctx->curve == KZGX_CURVE_BN254
+             ? msm_batch_impl<BN254G1, KZGX_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st)
+             : msm_batch_impl<BLS12381G1, KZGX_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf,
+                                                             st);
+}
+
+}  // namespace kzgx

@@ -1,0 +1,397 @@
+// Scalar-field (Fr) polynomial kernels for gfx950 -- the companion ops of
+// the prove path (reference: src/trusted_setup.cpp:214-225 and
+// src/util.cpp:172-284, NTL ZZ_pX arithmetic).
+//
+//  * k_quotient_single: q = (P - P(z)) / (X - z) and y = P(z) for a batch of
+//    openings, one wavefront per opening.  The recurrence
+//    q_{k-1} = p_k + z q_k is split into 64 lane chunks: local Horner sums,
+//    a 6-step wave scan of the carries (c_g += z^(L 2^s) c_{g+2^s}), then each
+//    lane replays its chunk from its carry-in.  Depth 2L + 6 mulmods instead
+//    of n.
+//  * k_poly_eval: Horner, one thread per evaluation point.
+//  * interpolation (polyfit): Z = prod (X - x_i) by a product tree, weights
+//    a_i = y_i / prod_{j != i}(x_i - x_j), power moments m_t = sum_i a_i x_i^t,
+//    and c_k = sum_{j > k} z_j m_{j-k-1}; every sum is a wavefront reduction.
+//    Result = the unique interpolant, identical to NTL's subproduct-tree fit.
+//
+// Canonical inputs are multiplied by Montgomery-form constants with fe_mul,
+// which yields canonical results (a * bR * R^-1 = ab), so no conversions are
+// needed on the streaming paths.
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "field.hpp"
+#include "kzgx_internal.hpp"
+
+namespace kzgx {
+
+template <class FR>
+KZGX_DEV Fe<FR> fe_shfl_down(const Fe<FR>& a, int d) {
+  Fe<FR> r;
+#pragma unroll
+  for (int i = 0; i < FR::N; i++) r.v[i] = __shfl_down(a.v[i], d, 64);
+  return r;
+}
+
+template <class FR>
+KZGX_DEV Fe<FR> fe_shfl_xor(const Fe<FR>& a, int m) {
+  Fe<FR> r;
+#pragma unroll
+  for (int i = 0; i < FR::N; i++) r.v[i] = __shfl_xor(a.v[i], m, 64);
+  return r;
+}
+
+template <class FR>
+KZGX_DEV Fe<FR> wave_sum(Fe<FR> a) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) a = fe_add<FR>(a, fe_shfl_xor<FR>(a, m));
+  return a;
+}
+
+template <class FR>
+KZGX_DEV Fe<FR> wave_prod(Fe<FR> a) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) a = fe_mul<FR>(a, fe_shfl_xor<FR>(a, m));
+  return a;
+}
+
+template <class FR>
+KZGX_DEV Fe<FR> fe_pow_u32(const Fe<FR>& base_m, uint32_t e) {
+  Fe<FR> acc = fe_one<FR>();
+  for (int b = 31; b >= 0; b--) {
+    acc = fe_sqr<FR>(acc);
+    if ((e >> b) & 1u) acc = fe_mul<FR>(acc, base_m);
+  }
+  return acc;
+}
+
+// --------------------------------------------------------------------------
+// single-opening quotient (create_proof(poly, z, 1), trusted_setup.cpp:214-225)
+// --------------------------------------------------------------------------
+template <class FR>
+__global__ __launch_bounds__(256) void k_quotient_single(const uint32_t* __restrict__ coeffs, uint32_t n,
+                                                         size_t cstride, const uint32_t* __restrict__ zs,
+                                                         uint32_t batch, uint32_t* __restrict__ q, size_t qstride,
+                                                         uint32_t* __restrict__ ys) {
+  constexpr int N = FR::N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= batch) return;  // whole wavefront
+  const uint32_t* P = coeffs + (size_t)j * cstride;
+  const Fe<FR> zm = fe_to_mont<FR>(fe_load<FR>(zs + (size_t)j * N));
+  const uint32_t L = (n + 63) / 64;
+  const uint32_t lo = min(lane * L, n), hi = min(lo + L, n);
+  // phase 1: local_g = sum_{k in chunk} p_k z^(k - lo)
+  Fe<FR> h = fe_zero<FR>();
+  for (uint32_t k = hi; k-- > lo;) h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+  // phase 2: c_g = sum_{u >= g} local_u z^(L (u - g))
+  Fe<FR> c = h;
+  Fe<FR> zp = fe_pow_u32<FR>(zm, L);
+#pragma unroll
+  for (int s = 0; s < 6; s++) {
+    Fe<FR> o = fe_shfl_down<FR>(c, 1 << s);
+    if (lane + (1u << s) < 64) c = fe_add<FR>(c, fe_mul<FR>(o, zp));  // canonical * Montgomery = canonical
+    zp = fe_sqr<FR>(zp);
+  }
+  Fe<FR> cin = fe_shfl_down<FR>(c, 1);
+  if (lane == 63) cin = fe_zero<FR>();
+  // phase 3: replay the chunk from its carry-in, emitting q_{k-1}
+  h = cin;
+  uint32_t* Q = q + (size_t)j * qstride;
+  for (uint32_t k = hi; k-- > lo;) {
+    h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+    if (k >= 1)
+      fe_store<FR>(Q + (size_t)(k - 1) * N, h);
+    else if (ys)
+      fe_store<FR>(ys + (size_t)j * N, h);
+  }
+  if (n == 0 && lane == 0 && ys) fe_store<FR>(ys + (size_t)j * N, fe_zero<FR>());
+}
+
+// --------------------------------------------------------------------------
+// evaluation at m points (evaluate_polynomial_points, util.cpp:186-211)
+// --------------------------------------------------------------------------
+template <class FR>
+__global__ __launch_bounds__(256) void k_poly_eval(const uint32_t* __restrict__ coeffs, uint32_t n,
+                                                   const uint32_t* __restrict__ xs, uint32_t m,
+                                                   uint32_t* __restrict__ ys) {
+  constexpr int N = FR::N;
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const Fe<FR> xm = fe_to_mont<FR>(fe_load<FR>(xs + (size_t)j * N));
+  Fe<FR> h = fe_zero<FR>();
+  for (uint32_t k = n; k-- > 0;) h = fe_add<FR>(fe_load<FR>(coeffs + (size_t)k * N), fe_mul<FR>(h, xm));
+  fe_store<FR>(ys + (size_t)j * N, h);
+}
+
+// --------------------------------------------------------------------------
+// interpolation (polyfit, util.cpp:172-184 / polyfit_R :213-248)
+// --------------------------------------------------------------------------
+template <class FR>
+__global__ void k_to_mont(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fe_store<FR>(out + (size_t)i * FR::N, fe_to_mont<FR>(fe_load<FR>(in + (size_t)i * FR::N)));
+}
+
+template <class FR>
+__global__ void k_from_mont(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fe_store<FR>(out + (size_t)i * FR::N, fe_from_mont<FR>(fe_load<FR>(in + (size_t)i * FR::N)));
+}
+
+// level 0 of the product tree: slot i = (X - x_i), 2 coefficients
+template <class FR>
+__global__ void k_tree_leaves(const uint32_t* __restrict__ xm, uint32_t n, uint32_t* __restrict__ lvl) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe_store<FR>(lvl + (size_t)(2 * i) * FR::N, fe_neg<FR>(fe_load<FR>(xm + (size_t)i * FR::N)));
+  fe_store<FR>(lvl + (size_t)(2 * i + 1) * FR::N, fe_one<FR>());
+}
+
+// level l -> l+1: slot j = slot 2j * slot 2j+1.  Input slots hold s+1
+// coefficients (s = 2^l nodes, fewer in the last slot: its degree is
+// cnt = min(s, n - j s)); one wavefront per output coefficient.
+template <class FR>
+__global__ __launch_bounds__(256) void k_tree_mul(const uint32_t* __restrict__ in, uint32_t s, uint32_t n,
+                                                  uint32_t* __restrict__ out, uint32_t nslots_out) {
+  constexpr int N = FR::N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t S = 2 * s;  // nodes per output slot
+  const uint64_t j = gw / (S + 1), k = gw % (S + 1);
+  if (j >= nslots_out) return;
+  const uint32_t base = (uint32_t)j * S;
+  const uint32_t da = min(s, n - base);                        // degree of left factor
+  const uint32_t db = base + s < n ? min(s, n - base - s) : 0;  // degree of right (0 -> constant 1)
+  const bool has_b = base + s < n;
+  const uint32_t* A = in + (size_t)(2 * j) * (s + 1) * N;
+  const uint32_t* B = in + (size_t)(2 * j + 1) * (s + 1) * N;
+  Fe<FR> acc = fe_zero<FR>();
+  if (k <= da + db) {
+    if (has_b) {
+      const uint32_t i0 = k > db ? (uint32_t)k - db : 0, i1 = min((uint32_t)k, da);
+      for (uint32_t i = i0 + lane; i <= i1; i += 64)
+        acc = fe_add<FR>(acc, fe_mul<FR>(fe_load<FR>(A + (size_t)i * N), fe_load<FR>(B + (size_t)(k - i) * N)));
+    } else if (lane == 0) {
+      acc = fe_load<FR>(A + (size_t)k * N);
+    }
+  }
+  acc = wave_sum<FR>(acc);
+  if (lane == 0) fe_store<FR>(out + ((size_t)j * (S + 1) + k) * N, acc);
+}
+
+// a_i = y_i / prod_{j != i} (x_i - x_j); one wavefront per node; flags duplicates
+template <class FR>
+__global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restrict__ xm, const uint32_t* __restrict__ ym,
+                                                        uint32_t n, uint32_t* __restrict__ a, uint32_t* err) {
+  constexpr int N = FR::N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const Fe<FR> xi = fe_load<FR>(xm + (size_t)i * N);
+  Fe<FR> p = fe_one<FR>();
+  for (uint32_t j = lane; j < n; j += 64)
+    if (j != i) p = fe_mul<FR>(p, fe_sub<FR>(xi, fe_load<FR>(xm + (size_t)j * N)));
+  p = wave_prod<FR>(p);
+  if (lane == 0) {
+    if (fe_is_zero<FR>(p)) atomicOr(err, 1u);
+    fe_store<FR>(a + (size_t)i * N, fe_mul<FR>(fe_load<FR>(ym + (size_t)i * N), fe_inv<FR>(p)));
+  }
+}
+
+// partial moments: part[it][t] = sum_{i in tile it} a_i x_i^t, t in [t0, t0+TT)
+constexpr int MOM_TT = 64;
+template <class FR>
+__global__ __launch_bounds__(256) void k_moments(const uint32_t* __restrict__ xm, const uint32_t* __restrict__ a,
+                                                 uint32_t n, uint32_t* __restrict__ part) {
+  constexpr int N = FR::N;
+  __shared__ uint32_t red[4][MOM_TT][N];
+  const uint32_t t0 = blockIdx.x * MOM_TT;
+  const uint32_t it = blockIdx.y;
+  const uint32_t i = it * 256 + threadIdx.x;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Fe<FR> x = fe_zero<FR>(), v = fe_zero<FR>();
+  if (i < n) {
+    x = fe_load<FR>(xm + (size_t)i * N);
+    // v = a_i x_i^t0: x_i^t0 via square-and-multiply
+    v = fe_mul<FR>(fe_load<FR>(a + (size_t)i * N), fe_pow_u32<FR>(x, t0));
+  }
+  for (int tt = 0; tt < MOM_TT; tt++) {
+    Fe<FR> s = wave_sum<FR>(v);
+    if (lane == 0) {
+#pragma unroll
+      for (int w = 0; w < N; w++) red[wave][tt][w] = s.v[w];
+    }
+    v = fe_mul<FR>(v, x);
+  }
+  __syncthreads();
+  if (threadIdx.x < MOM_TT && t0 + threadIdx.x < n) {
+    Fe<FR> s = fe_zero<FR>();
+    for (int w = 0; w < 4; w++) {
+      Fe<FR> o;
+#pragma unroll
+      for (int q = 0; q < N; q++) o.v[q] = red[w][threadIdx.x][q];
+      s = fe_add<FR>(s, o);
+    }
+    fe_store<FR>(part + ((size_t)it * n + t0 + threadIdx.x) * N, s);
+  }
+}
+
+template <class FR>
+__global__ void k_moments_sum(const uint32_t* __restrict__ part, uint32_t n, uint32_t ntiles, uint32_t* __restrict__ m) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  Fe<FR> s = fe_zero<FR>();
+  for (uint32_t it = 0; it < ntiles; it++) s = fe_add<FR>(s, fe_load<FR>(part + ((size_t)it * n + t) * FR::N));
+  fe_store<FR>(m + (size_t)t * FR::N, s);
+}
+
+// c_k = sum_{j=k+1}^{n} z_j m_{j-k-1}; one wavefront per coefficient; canonical out
+template <class FR>
+__global__ __launch_bounds__(256) void k_interp_coeffs(const uint32_t* __restrict__ Z, const uint32_t* __restrict__ m,
+                                                       uint32_t n, uint32_t* __restrict__ coeffs) {
+  constexpr int N = FR::N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;
+  Fe<FR> acc = fe_zero<FR>();
+  for (uint32_t j = k + 1 + lane; j <= n; j += 64)
+    acc = fe_add<FR>(acc, fe_mul<FR>(fe_load<FR>(Z + (size_t)j * N), fe_load<FR>(m + (size_t)(j - k - 1) * N)));
+  acc = wave_sum<FR>(acc);
+  if (lane == 0) fe_store<FR>(coeffs + (size_t)k * N, fe_from_mont<FR>(acc));
+}
+
+// --------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------
+template <class FR>
+static int quotient_single_impl(const uint32_t* d_coeffs, size_t n, size_t cstride, const uint32_t* d_z, size_t batch,
+                                uint32_t* d_q, size_t qstride, uint32_t* d_y, hipStream_t st) {
+  if (batch == 0) return KZGX_OK;
+  hipLaunchKernelGGL(k_quotient_single<FR>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, d_coeffs,
+                     (uint32_t)n, cstride, d_z, (uint32_t)batch, d_q, qstride, d_y);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int quotient_single(Ctx* ctx, const uint32_t* d_coeffs, size_t n, size_t coeff_stride_words, const uint32_t* d_z,
+                    size_t batch, uint32_t* d_q, size_t q_stride_words, uint32_t* d_y, hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254
+             ? quotient_single_impl<BN254Fr>(d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y, st)
+             : quotient_single_impl<BLS12381Fr>(d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y,
+                                                st);
+}
+
+template <class FR>
+static int poly_eval_impl(const uint32_t* d_coeffs, size_t n, const uint32_t* d_x, size_t m, uint32_t* d_y,
+                          hipStream_t st) {
+  if (m == 0) return KZGX_OK;
+  hipLaunchKernelGGL(k_poly_eval<FR>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, d_coeffs, (uint32_t)n, d_x,
+                     (uint32_t)m, d_y);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int poly_eval(Ctx* ctx, const uint32_t* d_coeffs, size_t n, const uint32_t* d_x, size_t m, uint32_t* d_y,
+              hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254 ? poly_eval_impl<BN254Fr>(d_coeffs, n, d_x, m, d_y, st)
+                                        : poly_eval_impl<BLS12381Fr>(d_coeffs, n, d_x, m, d_y, st);
+}
+
+template <class FR>
+static int interpolate_impl(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs, hipStream_t st) {
+  constexpr int N = FR::N;
+  const size_t eb = N * sizeof(uint32_t);
+  if (n == 0) return KZGX_OK;
+  // workspace: xm, ym, a, m (n each), Z-tree ping/pong (<= 2n + nslots), partials, err
+  size_t tiles = (n + 255) / 256;
+  size_t lvl_elems = 2 * n + 2;  // each level stores nslots * (s+1) <= n + nslots <= 2n coefficients
+  uint32_t *xm, *ym, *a, *mm, *L0, *L1, *part, *err;
+  size_t total = (4 * n + 2 * lvl_elems + tiles * n) * eb + 256;
+  char* base;
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws, total, &ctx->poly_ws_b));
+  base = (char*)ctx->d_poly_ws;
+  xm = (uint32_t*)base;
+  ym = xm + n * N;
+  a = ym + n * N;
+  mm = a + n * N;
+  L0 = mm + n * N;
+  L1 = L0 + lvl_elems * N;
+  part = L1 + lvl_elems * N;
+  err = part + tiles * n * N;
+  KZGX_TRY_HIP(hipMemsetAsync(err, 0, 4, st));
+  const unsigned g1 = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_to_mont<FR>, dim3(g1), dim3(256), 0, st, d_x, xm, (uint32_t)n);
+  hipLaunchKernelGGL(k_to_mont<FR>, dim3(g1), dim3(256), 0, st, d_y, ym, (uint32_t)n);
+  // product tree
+  hipLaunchKernelGGL(k_tree_leaves<FR>, dim3(g1), dim3(256), 0, st, xm, (uint32_t)n, L0);
+  uint32_t* cur = L0;
+  uint32_t* nxt = L1;
+  size_t s = 1;
+  while (s < n) {
+    size_t nslots_out = (n + 2 * s - 1) / (2 * s);
+    size_t waves = nslots_out * (2 * s + 1);
+    hipLaunchKernelGGL(k_tree_mul<FR>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, cur, (uint32_t)s,
+                       (uint32_t)n, nxt, (uint32_t)nslots_out);
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    s *= 2;
+  }
+  // cur: one slot of s+1 coefficients, Z has degree n (entries above n unused)
+  hipLaunchKernelGGL(k_interp_weights<FR>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, xm, ym, (uint32_t)n, a,
+                     err);
+  hipLaunchKernelGGL(k_moments<FR>, dim3((unsigned)((n + MOM_TT - 1) / MOM_TT), (unsigned)tiles), dim3(256), 0, st,
+                     xm, a, (uint32_t)n, part);
+  hipLaunchKernelGGL(k_moments_sum<FR>, dim3(g1), dim3(256), 0, st, part, (uint32_t)n, (uint32_t)tiles, mm);
+  hipLaunchKernelGGL(k_interp_coeffs<FR>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, cur, mm, (uint32_t)n,
+                     d_coeffs);
+  KZGX_TRY_HIP(hipGetLastError());
+  uint32_t h_err = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  return h_err ? KZGX_ERR_DIV_ZERO : KZGX_OK;
+}
+
+template <class FR>
+static int vanishing_impl(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipStream_t st) {
+  constexpr int N = FR::N;
+  const size_t eb = N * sizeof(uint32_t);
+  const size_t lvl_elems = 2 * n + 2;
+  char* base;
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws, (n + 2 * lvl_elems) * eb, &ctx->poly_ws_b));
+  base = (char*)ctx->d_poly_ws;
+  uint32_t* xm = (uint32_t*)base;
+  uint32_t* L0 = xm + n * N;
+  uint32_t* L1 = L0 + lvl_elems * N;
+  const unsigned g1 = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_to_mont<FR>, dim3(g1), dim3(256), 0, st, d_x, xm, (uint32_t)n);
+  hipLaunchKernelGGL(k_tree_leaves<FR>, dim3(g1), dim3(256), 0, st, xm, (uint32_t)n, L0);
+  uint32_t* cur = L0;
+  uint32_t* nxt = L1;
+  for (size_t s = 1; s < n; s *= 2) {
+    size_t nslots_out = (n + 2 * s - 1) / (2 * s);
+    size_t waves = nslots_out * (2 * s + 1);
+    hipLaunchKernelGGL(k_tree_mul<FR>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, cur, (uint32_t)s,
+                       (uint32_t)n, nxt, (uint32_t)nslots_out);
+    std::swap(cur, nxt);
+  }
+  hipLaunchKernelGGL(k_from_mont<FR>, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, cur, d_Z,
+                     (uint32_t)(n + 1));
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int poly_vanishing(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254 ? vanishing_impl<BN254Fr>(ctx, d_x, n, d_Z, st)
+                                        : vanishing_impl<BLS12381Fr>(ctx, d_x, n, d_Z, st);
+}
+
+int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
+                     hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254 ? interpolate_impl<BN254Fr>(ctx, d_x, d_y, n, d_coeffs, st)
+                                        : interpolate_impl<BLS12381Fr>(ctx, d_x, d_y, n, d_coeffs, st);
+}
+
+}  // namespace kzgx

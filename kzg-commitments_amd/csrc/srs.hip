@@ -1,0 +1,92 @@
+// SRS generation and small G1 helpers for gfx950.
+//
+// kzgx_gen_srs_g1 replaces the G1 half of trusted_setup(int)
+// (src/trusted_setup.cpp:21-74, worker generate_elements_range :123-135),
+// which computes power(s, i) per index and one PAIR_G1mul per point on
+// hardware_concurrency() std::threads.  Here every GPU thread derives
+// tau^(start+i) by square-and-multiply and runs its own fixed-base
+// double-and-add in XYZZ coordinates.
+#include <hip/hip_runtime.h>
+
+#include "curve.hpp"
+#include "kzgx_internal.hpp"
+
+namespace kzgx {
+
+template <class C>
+__global__ __launch_bounds__(256) void k_gen_srs(const uint32_t* __restrict__ tau_canon, uint64_t start, uint32_t n,
+                                                 uint32_t* __restrict__ out) {
+  using F = typename C::Fp;
+  using FR = typename C::Fr;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // e = tau^(start + i) mod r
+  const Fe<FR> tm = fe_to_mont<FR>(fe_load<FR>(tau_canon));
+  const uint64_t ex = start + i;
+  Fe<FR> e = fe_one<FR>();
+  for (int b = 63; b >= 0; b--) {
+    e = fe_sqr<FR>(e);
+    if ((ex >> b) & 1ull) e = fe_mul<FR>(e, tm);
+  }
+  e = fe_from_mont<FR>(e);
+  Affine<C> g;
+  g.x = fe_const<F>(C::GX);
+  g.y = fe_const<F>(C::GY);
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (int b = 8 * FR::N * 4 - 1; b >= 0; b--) {
+    acc = xyzz_dbl<C>(acc);
+    if ((e.v[b >> 5] >> (b & 31)) & 1u) acc = xyzz_add_affine<C>(acc, g);
+  }
+  Affine<C> a;
+  if (xyzz_to_affine<C>(acc, a)) {
+    a.x = fe_from_mont<F>(a.x);
+    a.y = fe_from_mont<F>(a.y);
+  }
+  affine_store<C>(out + (size_t)i * 2 * F::N, a);
+}
+
+// out = sum of count canonical affine points (zero or flagged = infinity)
+template <class C>
+__global__ void k_g1_sum(const uint32_t* __restrict__ xy, const uint32_t* __restrict__ inf, uint32_t count,
+                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  using F = typename C::Fp;
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t i = 0; i < count; i++) {
+    Affine<C> a = affine_load<C>(xy + (size_t)i * 2 * F::N);
+    if ((inf && inf[i]) || (fe_is_zero<F>(a.x) && fe_is_zero<F>(a.y))) continue;
+    a.x = fe_to_mont<F>(a.x);
+    a.y = fe_to_mont<F>(a.y);
+    acc = xyzz_add_affine<C>(acc, a);
+  }
+  Affine<C> r;
+  bool fin = xyzz_to_affine<C>(acc, r);
+  if (fin) {
+    r.x = fe_from_mont<F>(r.x);
+    r.y = fe_from_mont<F>(r.y);
+  }
+  affine_store<C>(out, r);
+  *out_inf = fin ? 0u : 1u;
+}
+
+int gen_srs_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, uint32_t* d_out, hipStream_t st) {
+  dim3 blk(256), grd((unsigned)((n + 255) / 256));
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_gen_srs<BN254G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, d_out);
+  else
+    hipLaunchKernelGGL(k_gen_srs<BLS12381G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, d_out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int g1_sum(Ctx* ctx, const uint32_t* d_xy, const uint32_t* d_inf, size_t count, uint32_t* d_out, uint32_t* d_out_inf,
+           hipStream_t st) {
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g1_sum<BN254G1>, dim3(1), dim3(64), 0, st, d_xy, d_inf, (uint32_t)count, d_out, d_out_inf);
+  else
+    hipLaunchKernelGGL(k_g1_sum<BLS12381G1>, dim3(1), dim3(64), 0, st, d_xy, d_inf, (uint32_t)count, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+}  // namespace kzgx

@@ -1,0 +1,205 @@
+"""ctypes binding of libkzgx.so (the C ABI in include/kzg_gpu.h).
+
+Host-side plumbing for tests and bench.py: numpy arrays in, numpy arrays out.
+There is no fallback: if libkzgx.so is missing or no gfx950 device is visible,
+every entry point raises.  Scalars are (n, 4) uint64 arrays (little-endian
+limbs, canonical mod r); points are (n, 2 * W64) uint64 arrays (x || y,
+canonical), W64 = 4 (BN254) or 6 (BLS12-381), infinity = all zeros.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libkzgx.so")
+CURVES = {"BN254": 0, "BLS12381": 1}
+BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
+
+# exported C symbols (must match include/kzg_gpu.h)
+EXPORTS = [
+    "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
+    "kzgx_srs_size", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
+    "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_poly_eval",
+    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_sum",
+]
+
+_lib = None
+u64p = ctypes.POINTER(ctypes.c_uint64)
+intp = ctypes.POINTER(ctypes.c_int)
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+
+
+class KzgxError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        self.status = status
+        super().__init__("%s: %s (%d)" % (where, lib().kzgx_strerror(status).decode(), status))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libkzgx.so not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "kzgx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+            "kzgx_base_limbs": (ctypes.c_int, [ctypes.c_int]),
+            "kzgx_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int]),
+            "kzgx_destroy": (None, [vp]),
+            "kzgx_sync": (ctypes.c_int, [vp]),
+            "kzgx_curve": (ctypes.c_int, [vp]),
+            "kzgx_srs_size": (sz, [vp]),
+            "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
+            "kzgx_gen_srs_g1": (ctypes.c_int, [vp, u64p, sz, sz]),
+            "kzgx_get_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
+            "kzgx_msm_g1": (ctypes.c_int, [vp, u64p, sz, u64p, intp]),
+            "kzgx_msm_g1_batch": (ctypes.c_int, [vp, u64p, sz, sz, u64p, intp]),
+            "kzgx_msm_g1_batch_device": (ctypes.c_int, [vp, vp, sz, sz, sz, vp, vp, vp]),
+            "kzgx_quotient_single_batch_device": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, vp, sz, vp, vp]),
+            "kzgx_prove_single_batch": (ctypes.c_int, [vp, u64p, sz, sz, u64p, sz, u64p, intp, u64p]),
+            "kzgx_prove_single_batch_device": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, vp, vp, vp, vp]),
+            "kzgx_poly_eval": (ctypes.c_int, [vp, u64p, sz, u64p, sz, u64p]),
+            "kzgx_poly_interpolate": (ctypes.c_int, [vp, u64p, u64p, sz, u64p]),
+            "kzgx_poly_vanishing": (ctypes.c_int, [vp, u64p, sz, u64p]),
+            "kzgx_g1_sum": (ctypes.c_int, [vp, u64p, intp, sz, u64p, intp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(u64p)
+
+
+def _chk(rc, where):
+    if rc != 0:
+        raise KzgxError(rc, where)
+
+
+def as_scalars(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+
+
+class Context:
+    """One device context (SRS + stream + workspaces), kzgx_ctx*."""
+
+    def __init__(self, curve: str = "BN254", device: int = 0):
+        self.curve = curve
+        self.w64 = BASE_LIMBS[curve]
+        h = vp()
+        _chk(lib().kzgx_create(ctypes.byref(h), CURVES[curve], device), "kzgx_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kzgx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- SRS ----
+    @property
+    def srs_size(self) -> int:
+        return lib().kzgx_srs_size(self.h)
+
+    def load_srs(self, xy: np.ndarray):
+        xy = np.ascontiguousarray(xy, dtype=np.uint64).reshape(-1, 2 * self.w64)
+        _chk(lib().kzgx_load_srs_g1(self.h, _p(xy), xy.shape[0]), "kzgx_load_srs_g1")
+
+    def gen_srs(self, tau: int, n: int, start: int = 0):
+        t = np.array([(tau >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+        _chk(lib().kzgx_gen_srs_g1(self.h, _p(t), start, n), "kzgx_gen_srs_g1")
+
+    def get_srs(self, n: int | None = None) -> np.ndarray:
+        n = self.srs_size if n is None else n
+        out = np.zeros((n, 2 * self.w64), dtype=np.uint64)
+        _chk(lib().kzgx_get_srs_g1(self.h, _p(out), n), "kzgx_get_srs_g1")
+        return out
+
+    # ---- MSM ----
+    def msm_batch(self, scalars: np.ndarray, n: int, batch: int):
+        sc = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1)
+        assert sc.size >= n * batch * 4
+        out = np.zeros((batch, 2 * self.w64), dtype=np.uint64)
+        inf = np.zeros(batch, dtype=np.int32)
+        _chk(lib().kzgx_msm_g1_batch(self.h, _p(sc) if n else None, n, batch, _p(out),
+                                     inf.ctypes.data_as(intp)), "kzgx_msm_g1_batch")
+        return out, inf.astype(bool)
+
+    def msm(self, scalars: np.ndarray):
+        sc = as_scalars(scalars)
+        out, inf = self.msm_batch(sc, sc.shape[0], 1)
+        return out[0], bool(inf[0])
+
+    def msm_batch_device(self, d_scalars: int, n: int, batch: int, stride: int, d_out: int, d_inf: int,
+                         stream: int | None = None):
+        _chk(lib().kzgx_msm_g1_batch_device(self.h, d_scalars, n, batch, stride, d_out, d_inf, stream),
+             "kzgx_msm_g1_batch_device")
+
+    # ---- proofs ----
+    def prove_single_batch(self, coeffs: np.ndarray, zs: np.ndarray, shared: bool = True):
+        """coeffs: (n, 4) shared polynomial (shared=True) or (batch, n, 4)."""
+        zs = as_scalars(zs)
+        batch = zs.shape[0]
+        c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+        n = c.shape[-2] if c.ndim >= 2 else 0
+        stride = 0 if shared else n
+        out = np.zeros((batch, 2 * self.w64), dtype=np.uint64)
+        inf = np.zeros(batch, dtype=np.int32)
+        y = np.zeros((batch, 4), dtype=np.uint64)
+        _chk(lib().kzgx_prove_single_batch(self.h, _p(c) if n else None, n, stride, _p(zs), batch, _p(out),
+                                           inf.ctypes.data_as(intp), _p(y)), "kzgx_prove_single_batch")
+        return out, inf.astype(bool), y
+
+    def prove_single_batch_device(self, d_coeffs, n, stride, d_z, batch, d_out, d_inf, d_y=None, stream=None):
+        _chk(lib().kzgx_prove_single_batch_device(self.h, d_coeffs, n, stride, d_z, batch, d_out, d_inf, d_y,
+                                                  stream), "kzgx_prove_single_batch_device")
+
+    def quotient_single_device(self, d_coeffs, n, stride, d_z, batch, d_q, q_stride, d_y=None, stream=None):
+        _chk(lib().kzgx_quotient_single_batch_device(self.h, d_coeffs, n, stride, d_z, batch, d_q, q_stride, d_y,
+                                                     stream), "kzgx_quotient_single_batch_device")
+
+    # ---- poly ----
+    def poly_eval(self, coeffs: np.ndarray, xs: np.ndarray) -> np.ndarray:
+        c = as_scalars(coeffs) if len(coeffs) else np.zeros((0, 4), dtype=np.uint64)
+        x = as_scalars(xs)
+        y = np.zeros_like(x)
+        _chk(lib().kzgx_poly_eval(self.h, _p(c) if c.shape[0] else None, c.shape[0], _p(x), x.shape[0], _p(y)),
+             "kzgx_poly_eval")
+        return y
+
+    def interpolate(self, xs: np.ndarray, ys: np.ndarray) -> np.ndarray:
+        x = as_scalars(xs)
+        y = as_scalars(ys)
+        out = np.zeros_like(x)
+        _chk(lib().kzgx_poly_interpolate(self.h, _p(x), _p(y), x.shape[0], _p(out)), "kzgx_poly_interpolate")
+        return out
+
+    def vanishing(self, xs: np.ndarray) -> np.ndarray:
+        x = as_scalars(xs)
+        out = np.zeros((x.shape[0] + 1, 4), dtype=np.uint64)
+        _chk(lib().kzgx_poly_vanishing(self.h, _p(x) if x.shape[0] else None, x.shape[0], _p(out)),
+             "kzgx_poly_vanishing")
+        return out
+
+    def g1_sum(self, pts: np.ndarray, inf=None):
+        pts = np.ascontiguousarray(pts, dtype=np.uint64).reshape(-1, 2 * self.w64)
+        f = None if inf is None else np.ascontiguousarray(inf, dtype=np.int32)
+        out = np.zeros(2 * self.w64, dtype=np.uint64)
+        oi = ctypes.c_int(0)
+        _chk(lib().kzgx_g1_sum(self.h, _p(pts), None if f is None else f.ctypes.data_as(intp), pts.shape[0],
+                               _p(out), ctypes.byref(oi)), "kzgx_g1_sum")
+        return out, bool(oi.value)

@@ -1,0 +1,169 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact: affine (x, y) of a group element is unique, so every comparison is
+exact equality of canonical integers.  Sizes are chosen so the oracle side
+finishes in seconds; full-size cases use the MSM-independent identity
+commit == [P(tau)]G1."""
+import numpy as np
+import pytest
+
+import kzg_ref as K
+
+pytestmark = pytest.mark.gpu
+
+CURVES = [("BN254", K.BN254), ("BLS12381", K.BLS12381)]
+
+
+def limbs(vals, nl=4):
+    import corc
+    return corc.ints_to_limbs(vals, nl)
+
+
+def pt(curve, row, inf=False):
+    import corc
+    return None if inf else corc.array_to_points(curve, row[None, :])[0]
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_gen_srs_matches_oracle(name, C, ctx_factory, oracle_c):
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    ctx.gen_srs(tau, 97, start=5)
+    got = ctx.get_srs(97)
+    ref = oracle_c.gen_srs(name, tau, 102)[5:]
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 129, 600])
+def test_msm_matches_naive(name, C, n, ctx_factory, oracle_c):
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    srs = oracle_c.gen_srs(name, tau, max(n, 2))
+    ctx.load_srs(srs)
+    sc = K.random_scalars(C, n, seed=1000 + n)
+    if n >= 3:
+        sc[0], sc[1], sc[2] = 0, 1, C.r - 1
+    S = limbs(sc)
+    out, inf = ctx.msm(S)
+    ref = oracle_c.msm_naive(name, srs, S)
+    assert pt(name, out, inf) == ref
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_msm_batch_identity(name, C, ctx_factory):
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    n, batch = 4097, 6
+    ctx.gen_srs(tau, 5000)
+    polys = [K.random_scalars(C, n, seed=77 + b) for b in range(batch)]
+    polys[1] = [0] * n                       # zero polynomial -> infinity
+    polys[2] = [5] + [0] * (n - 1)           # constant
+    S = np.concatenate([limbs(p) for p in polys])
+    out, inf = ctx.msm_batch(S, n, batch)
+    for b in range(batch):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("tau", [0, 1, 2, -1])
+def test_degenerate_srs(name, C, tau, ctx_factory, oracle_c):
+    """tau = 0 gives infinite SRS points, tau = +-1 repeats points (bucket doublings)."""
+    ctx = ctx_factory(name)
+    t = tau % C.r
+    n = 300
+    srs = oracle_c.gen_srs(name, t, n)
+    ctx.load_srs(srs)
+    sc = K.random_scalars(C, n, seed=5)
+    sc[7] = sc[3]
+    out, inf = ctx.msm(limbs(sc))
+    assert pt(name, out, inf) == K.commit_via_tau(C, t, sc)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_empty_msm_is_infinity(name, C, ctx_factory):
+    ctx = ctx_factory(name)
+    ctx.gen_srs(K.default_tau(C), 8)
+    out, inf = ctx.msm_batch(np.zeros((0, 4), dtype=np.uint64), 0, 2)
+    assert inf.all() and not out.any()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [1, 2, 5, 64, 65, 130, 4097])
+def test_single_opening_proofs(name, C, n, ctx_factory):
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    ctx.gen_srs(tau, max(n + 1, 8))
+    P = K.random_scalars(C, n, seed=n)
+    zs = [0, 1, 7, n + 3, C.r - 2]
+    out, inf, y = ctx.prove_single_batch(limbs(P), limbs(zs))
+    for j, z in enumerate(zs):
+        q = K.proof_quotient(C, P, z, 1) if z < 2**31 else None
+        yv = K.poly_eval(C, P, z)
+        assert int(sum(int(y[j, i]) << (64 * i) for i in range(4))) == yv
+        # q(tau) = (P(tau) - P(z)) / (tau - z)
+        qt = (K.poly_eval(C, P, tau) - yv) * pow((tau - z) % C.r, -1, C.r) % C.r
+        exp = K.scalar_mul(C, (C.gx, C.gy), qt)
+        assert pt(name, out[j], inf[j]) == exp, (n, z)
+        if q is not None and n < 200:
+            assert pt(name, out[j], inf[j]) == K.commit_via_tau(C, tau, q)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_prove_batch_distinct_polys(name, C, ctx_factory):
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    n, batch = 513, 5
+    ctx.gen_srs(tau, n + 1)
+    polys = [K.random_scalars(C, n, seed=300 + b) for b in range(batch)]
+    zs = [b * 11 for b in range(batch)]
+    coeffs = np.stack([limbs(p) for p in polys])
+    out, inf, y = ctx.prove_single_batch(coeffs, limbs(zs), shared=False)
+    for b in range(batch):
+        q = K.proof_quotient(C, polys[b], zs[b], 1)
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, q)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [1, 2, 9, 100, 257])
+def test_poly_eval_and_interpolate(name, C, n, ctx_factory, oracle_c):
+    ctx = ctx_factory(name)
+    P = K.random_scalars(C, n, seed=n + 9)
+    xs = [i + 3 for i in range(n)]
+    ys = ctx.poly_eval(limbs(P), limbs(xs))
+    assert oracle_c.limbs_to_ints(ys) == [K.poly_eval(C, P, x) for x in xs]
+    coeffs = ctx.interpolate(limbs(xs), ys)
+    got = oracle_c.limbs_to_ints(coeffs)
+    assert got == P + [0] * (n - len(P))
+    # arbitrary nodes + values (signed-char style residues)
+    xs2 = K.random_scalars(C, n, seed=4 * n)
+    ys2 = [(-(i % 200)) % C.r for i in range(n)]
+    got2 = oracle_c.limbs_to_ints(ctx.interpolate(limbs(xs2), limbs(ys2)))
+    ref2 = oracle_c.interpolate(name, xs2, ys2)
+    assert K.normalize(got2) == ref2
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_interpolate_duplicate_node_raises(name, C, ctx_factory):
+    import kzgx
+    ctx = ctx_factory(name)
+    with pytest.raises(kzgx.KzgxError):
+        ctx.interpolate(limbs([1, 2, 1]), limbs([3, 4, 5]))
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_g1_sum(name, C, ctx_factory, oracle_c):
+    ctx = ctx_factory(name)
+    srs = oracle_c.gen_srs(name, 3, 6)
+    out, inf = ctx.g1_sum(srs)
+    exp = K.scalar_mul(C, (C.gx, C.gy), 1 + 3 + 9 + 27 + 81 + 243)
+    assert pt(name, out, inf) == exp
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 9, 64, 100, 257])
+def test_vanishing(name, C, n, ctx_factory, oracle_c):
+    ctx = ctx_factory(name)
+    xs = K.random_scalars(C, n, seed=n)
+    got = oracle_c.limbs_to_ints(ctx.vanishing(limbs(xs)))
+    assert got == K.linear_roots(C, xs)
