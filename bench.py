@@ -1,0 +1,316 @@
+#!/usr/bin/env python3
+"""bench.py -- KZG commits/s + proofs/s on MI355X (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1]): BN254 (miracl Nogami curve),
+degree 4096 -> 4097 coefficients per polynomial, SRS of 5000 points
+(reference benchmark/benchmark.cpp:111).  One "step" = one batch of B
+polynomials per GPU, each committed (create_commit: MSM over 4097 points)
+and opened at one point (create_proof(poly, z, 1): quotient + MSM over 4096
+points), i.e. 2B commits+proofs per GPU per step, all inputs resident in HBM
+before the timed region.  Multi-GPU = independent batches per rank (weak
+scaling, no collective in the data path); timing is max over ranks.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --workload cfg2|cfg3|cfg4]
+
+Prints ONE JSON line on rank 0.  The roofline entry is for the dominant
+kernel (msm_accum), timed with HIP events on its launch stream inside the
+timed region.  cpu_baseline times the C oracle (oracle/liboracle.so, a
+restatement of the reference's naive per-term polyeval_G1) on a bounded
+sample on one host core.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kzg-commitments_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+REF_COMMIT_S = 1.104637  # README.md:132, BN254 degree 4096, 1 thread, unstated CPU
+REF_PROOF_S = 1.080747
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="polynomials per GPU per step")
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4"])
+    ap.add_argument("--cpu-sample", type=int, default=3, help="commits (+ as many proofs) timed on the CPU oracle")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def curve_consts(curve):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))  # checker only (parity + cpu_baseline)
+    import kzg_ref
+    return kzg_ref, kzg_ref.CURVES[curve]
+
+
+def random_fr(rng, shape, r):
+    """uniform integers in [0, r) as little-endian uint64 limbs (..., 4)"""
+    rl = [(r >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)]
+    top_bits = r.bit_length() - 192
+    out = rng.integers(0, 2**64, size=shape + (4,), dtype=np.uint64)
+    out[..., 3] &= np.uint64((1 << top_bits) - 1)
+    while True:
+        w = out.reshape(-1, 4)
+        ge = np.zeros(w.shape[0], dtype=bool)
+        eq = np.ones(w.shape[0], dtype=bool)
+        for i in (3, 2, 1, 0):
+            ge |= eq & (w[:, i] > np.uint64(rl[i]))
+            eq &= w[:, i] == np.uint64(rl[i])
+        ge |= eq
+        if not ge.any():
+            return out
+        fresh = rng.integers(0, 2**64, size=(int(ge.sum()), 4), dtype=np.uint64)
+        fresh[:, 3] &= np.uint64((1 << top_bits) - 1)
+        w[ge] = fresh
+
+
+def to_int(row):
+    return sum(int(row[i]) << (64 * i) for i in range(len(row)))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import kzgx
+
+    curve = "BLS12381" if args.workload == "cfg4" else "BN254"
+    K, C = curve_consts(curve)
+    tau = K.default_tau(C)
+    degree = 4096
+    n = degree + 1
+    B = args.batch
+    ctx = kzgx.Context(curve, device=local)
+    ctx.gen_srs(tau, 5000)
+    w64 = ctx.w64
+
+    rng = np.random.default_rng(0x4B5A47 + rank)
+    if args.workload == "cfg3":
+        # one degree-4096 polynomial opened at x = 0..B-1 (reference multi-proof
+        # benchmark's 4096 openings, as single-opening proofs)
+        coeffs_h = random_fr(rng, (1, n), C.r)
+        zs_h = np.zeros((B, 4), dtype=np.uint64)
+        zs_h[:, 0] = np.arange(B, dtype=np.uint64)
+    else:
+        coeffs_h = random_fr(rng, (B, n), C.r)
+        zs_h = np.zeros((B, 4), dtype=np.uint64)
+        zs_h[:, 0] = np.arange(B, dtype=np.uint64) % n
+    d_coeffs = torch.from_numpy(coeffs_h.view(np.int64)).to(dev)
+    d_z = torch.from_numpy(zs_h.view(np.int64)).to(dev)
+    d_cout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
+    d_cinf = torch.zeros((B,), dtype=torch.int32, device=dev)
+    d_pout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
+    d_pinf = torch.zeros((B,), dtype=torch.int32, device=dev)
+    d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    sp = stream.cuda_stream
+    cstride = 0 if args.workload == "cfg3" else n
+
+    def step():
+        if args.workload != "cfg3":
+            ctx.msm_batch_device(d_coeffs.data_ptr(), n, B, n, d_cout.data_ptr(), d_cinf.data_ptr(), sp)
+        ctx.prove_single_batch_device(d_coeffs.data_ptr(), n, cstride, d_z.data_ptr(), B, d_pout.data_ptr(),
+                                      d_pinf.data_ptr(), d_y.data_ptr(), sp)
+
+    units_per_step = B if args.workload == "cfg3" else 2 * B
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ctx.prof_clear()
+    ctx.prof_enable(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ctx.prof_enable(False)
+    elapsed = t1 - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    kern = {}
+    for name in ("msm_count", "msm_scan", "msm_scatter", "msm_accum", "msm_reduce", "quotient_single"):
+        ms, cnt = ctx.prof_read(name)
+        kern[name] = (ms, cnt)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- parity spot check (oracle identity, MSM-independent) ----
+    checked = ok = 0
+    if rank == 0:
+        cout = d_cout.cpu().numpy().view(np.uint64)
+        cinf = d_cinf.cpu().numpy()
+        pout = d_pout.cpu().numpy().view(np.uint64)
+        pinf = d_pinf.cpu().numpy()
+        G = (C.gx, C.gy)
+        for b in (0, B - 1):
+            pb = 0 if args.workload == "cfg3" else b
+            P = [to_int(row) for row in coeffs_h[pb]]
+            ptau = K.poly_eval(C, P, tau)
+            if args.workload != "cfg3":
+                exp = K.scalar_mul(C, G, ptau)
+                got = None if cinf[b] else (to_int(cout[b, :w64]), to_int(cout[b, w64:]))
+                checked += 1
+                ok += exp == got
+            z = to_int(zs_h[b])
+            qt = (ptau - K.poly_eval(C, P, z)) * pow((tau - z) % C.r, -1, C.r) % C.r
+            exp = K.scalar_mul(C, G, qt)
+            got = None if pinf[b] else (to_int(pout[b, :w64]), to_int(pout[b, w64:]))
+            checked += 1
+            ok += exp == got
+
+    # ---- CPU baseline (rank 0, N = 1 only) ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
+        import corc
+        corc.build()
+        srs = corc.gen_srs(curve, tau, n)
+        s = args.cpu_sample
+        polys = [coeffs_h[0 if args.workload == "cfg3" else i] for i in range(s)]
+        tc0 = time.perf_counter()
+        nunits = 0
+        for i in range(s):
+            P = [to_int(row) for row in polys[i]]
+            if args.workload != "cfg3":
+                corc.msm_naive(curve, srs, polys[i])  # create_commit
+                nunits += 1
+            q = K.proof_quotient(C, P, int(zs_h[i, 0]), 1)
+            corc.msm_naive(curve, srs[: max(len(q), 1)], corc.ints_to_limbs(q, 4))  # create_proof
+            nunits += 1
+        tcpu = time.perf_counter() - tc0
+        cpu_model = platform.processor()
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("model name"):
+                        cpu_model = line.split(":", 1)[1].strip()
+                        break
+        except OSError:
+            pass
+        cpu = {
+            "value": nunits / tcpu,
+            "unit": "commits+proofs/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": "%d %s at degree %d on the C restatement of the reference's naive per-term polyeval_G1 "
+                      "(oracle/kzg_oracle.c), 1 thread, %s, %.1f s" % (
+                          nunits, "proofs" if args.workload == "cfg3" else "commits+proofs", degree, cpu_model,
+                          tcpu),
+        }
+
+    if rank == 0:
+        acc_ms, acc_cnt = kern["msm_accum"]
+        # algorithmic bytes per MSM unit: n (affine point + 32 B scalar) + affine out
+        P_b = 2 * w64 * 8
+        unit_bytes_commit = n * (P_b + 32) + P_b
+        unit_bytes_proof = (n - 1) * (P_b + 32) + P_b
+        per_step_bytes = B * unit_bytes_proof + (0 if args.workload == "cfg3" else B * unit_bytes_commit)
+        launches_per_step = 1 if args.workload == "cfg3" else 2
+        bytes_per_launch = per_step_bytes / launches_per_step
+        avg_launch_ms = acc_ms / max(acc_cnt, 1)
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if acc_cnt else None
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
+        if os.path.exists(tpath):
+            try:
+                with open(tpath) as f:
+                    tj = json.load(f)
+                if tj.get("batch") == B:
+                    traffic = tj.get("msm_accum_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        total_units = units_per_step * args.steps * world
+        value = total_units / elapsed
+        madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * ctx_windows(ctx)
+        line = {
+            "metric": "KZG commits/sec + proofs/sec, %s degree-4096" % curve,
+            "value": value,
+            "unit": "commits+proofs/s" if args.workload != "cfg3" else "proofs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / (2.0 / (REF_COMMIT_S + REF_PROOF_S))) if args.workload == "cfg2" else None,
+            "dtype": "uint32 limbs (254-bit Montgomery Fp)" if curve == "BN254" else "uint32 limbs (381-bit Montgomery Fp)",
+            "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 from fixed tau",
+            "config": {
+                "workload": {"cfg2": "BN254 degree-4096 commit + single-opening proof, batched",
+                             "cfg3": "BN254 degree-4096 poly, batched single-opening proofs at x=0..B-1",
+                             "cfg4": "BLS12-381 degree-4096 commit + single-opening proof, batched"}[args.workload],
+                "curve": curve,
+                "degree": degree,
+                "batch_per_gpu": B,
+                "srs_points": 5000,
+                "parallelism": "dp%d (independent batches, no collective)" % world,
+            },
+            "roofline": {
+                "kernel": "msm_accum",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "avg_launch_ms": avg_launch_ms,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "note": "integer-VALU bound (no MFMA); see secondary",
+            },
+            "secondary": {
+                "msm_accum_mixed_adds_per_s": madds / (acc_ms * 1e-3 / max(acc_cnt, 1) * launches_per_step)
+                if acc_cnt else None,
+                "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
+                "event_ms_total": ev_ms,
+            },
+            "parity": {"checked": checked, "ok": int(ok), "method": "[P(tau)]G1 / [q(tau)]G1 identity"},
+            "cpu_baseline": cpu,
+            "reference_published": {"commits_per_s": 1 / REF_COMMIT_S, "proofs_per_s": 1 / REF_PROOF_S,
+                                    "source": "README.md:132 (unstated CPU, 1 thread)"},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def ctx_windows(ctx):
+    c = 10
+    return (257 + c - 1) // c
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,16 @@ void kzgx_destroy(kzgx_ctx* ctx);
 int kzgx_sync(kzgx_ctx* ctx);
 int kzgx_curve(const kzgx_ctx* ctx);
 size_t kzgx_srs_size(const kzgx_ctx* ctx);
+/* the context's own HIP stream (hipStream_t), used when stream == NULL */
+void* kzgx_stream(kzgx_ctx* ctx);
+
+/* per-kernel timing: when enabled, every launch of a named kernel
+ * ("msm_count", "msm_scan", "msm_scatter", "msm_accum", "msm_reduce",
+ * "quotient_single") is bracketed by HIP events on its launch stream;
+ * kzgx_prof_read sums (and then drops) the records of one name. */
+int kzgx_prof_enable(kzgx_ctx* ctx, int on);
+int kzgx_prof_read(kzgx_ctx* ctx, const char* name, double* total_ms, int* count);
+int kzgx_prof_clear(kzgx_ctx* ctx);
 
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */

@@ -1,200 +1,210 @@
-// G1 arithmetic on y^2 = x^3 + b (a = 0) for gfx950.
+// G1 arithmetic on y^2 = x^3 + b (a = 0) for gfx950, over the radix-2^29
+// lazily reduced base field of field29.hpp.
 //
 // Bucket accumulators use extended Jacobian "XYZZ" coordinates
 // (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2): a mixed add with an affine SRS point
-// costs 8M + 2S and a full add 12M + 2S, with no inversion.  ZZ == 0 marks
-// infinity.  All formulas are complete over the special cases (P == Q ->
+// costs 8M + 2S and a full add 12M + 2S, with no inversion.  ZZ == 0 (exact
+// zero limbs) marks infinity; every path that yields infinity writes it
+// exactly.  The formulas are complete over the special cases (P == Q ->
 // doubling, P == -Q -> infinity), so the result is the exact group element
 // whatever the SRS (tau = 0 / 1 / -1 included).
+//
+// Value bounds (m = field modulus; products are < 2m, see field29.hpp):
+//   affine x, y (table / inputs)     < m   (canonical Montgomery)
+//   XYZZ X < 8m, Y < 4m, ZZ, ZZZ < 2m   (invariant kept by every op below)
+// Each subtraction adds the smallest multiple of m that keeps it
+// non-negative; every product's operands satisfy a b < 222 m^2 (BN254, the
+// tighter of the two curves).
 //
 // Replaces miracl-core's ECP_add / PAIR_G1mul on the hot path
 // (src/trusted_setup.cpp:161-170).
 #pragma once
 #include "field.hpp"
+#include "field29.hpp"
 
-// Point operations are real calls (not inlined): each is 8-14 inlined field
-// products, and inlining them into every kernel call site multiplies code
-// size (and compile time) without helping the scheduler.
+// Cold or non-critical point operations are real calls (not inlined):
+// inlining them into every call site multiplies code size (and compile
+// time) without helping the scheduler.  The hot loop uses the _impl forms.
 #define KZGX_PT __device__ __noinline__
 
 namespace kzgx {
 
 template <class C>
-struct Affine;
-template <class C>
-struct Xyzz;
-template <class C>
-KZGX_PT Xyzz<C> xyzz_dbl_affine(const Affine<C>& a);
-template <class C>
-KZGX_PT Xyzz<C> xyzz_dbl(const Xyzz<C>& p);
-template <class C>
-KZGX_PT Xyzz<C> xyzz_add_affine(const Xyzz<C>& p, const Affine<C>& a);
-template <class C>
-KZGX_PT Xyzz<C> xyzz_add(const Xyzz<C>& p, const Xyzz<C>& q);
-template <class C>
-KZGX_PT bool xyzz_to_affine(const Xyzz<C>& p, Affine<C>& out);
-
-template <class C>
 struct Affine {
-  Fe<typename C::Fp> x, y;
+  F29<typename C::Fp29> x, y;
 };
 
 template <class C>
 struct Xyzz {
-  Fe<typename C::Fp> X, Y, ZZ, ZZZ;
+  F29<typename C::Fp29> X, Y, ZZ, ZZZ;
 };
+
+// words per stored affine point / XYZZ point (16-byte aligned)
+template <class C>
+constexpr int affine_words() {
+  return (2 * C::Fp29::L + 3) & ~3;
+}
+template <class C>
+constexpr int xyzz_words() {
+  return 4 * C::Fp29::L;
+}
+
+template <class C>
+KZGX_PT Xyzz<C> xyzz_dbl(const Xyzz<C>& p);
+template <class C>
+KZGX_PT Xyzz<C> xyzz_dbl_affine(const Affine<C>& a);
 
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_inf() {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   Xyzz<C> r;
-  r.X = fe_one<F>();
-  r.Y = fe_one<F>();
-  r.ZZ = fe_zero<F>();
-  r.ZZZ = fe_zero<F>();
+  r.X = f29_one<F>();
+  r.Y = f29_one<F>();
+  r.ZZ = f29_zero<F>();
+  r.ZZZ = f29_zero<F>();
   return r;
 }
 
 template <class C>
 KZGX_DEV bool xyzz_is_inf(const Xyzz<C>& p) {
-  return fe_is_zero<typename C::Fp>(p.ZZ);
+  return f29_is_zero_exact<typename C::Fp29>(p.ZZ);
 }
 
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_from_affine(const Affine<C>& a) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   Xyzz<C> r;
   r.X = a.x;
   r.Y = a.y;
-  r.ZZ = fe_one<F>();
-  r.ZZZ = fe_one<F>();
+  r.ZZ = f29_one<F>();
+  r.ZZZ = f29_one<F>();
   return r;
 }
 
-// doubling of an affine point (mdbl-2008-s-1)
+// doubling of an affine point (mdbl-2008-s-1); x, y < 2m
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_dbl_affine_impl(const Affine<C>& a) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   Xyzz<C> r;
-  Fe<F> U = fe_dbl<F>(a.y);
-  Fe<F> V = fe_sqr<F>(U);
-  Fe<F> W = fe_mul<F>(U, V);
-  Fe<F> S = fe_mul<F>(a.x, V);
-  Fe<F> xx = fe_sqr<F>(a.x);
-  Fe<F> M = fe_add<F>(fe_dbl<F>(xx), xx);
-  Fe<F> X3 = fe_sub<F>(fe_sqr<F>(M), fe_dbl<F>(S));
-  r.Y = fe_sub<F>(fe_mul<F>(M, fe_sub<F>(S, X3)), fe_mul<F>(W, a.y));
+  F29<F> U = f29_add<F>(a.y, a.y);                      // < 4m
+  F29<F> V = f29_sqr<F>(U);                             // < 2m
+  F29<F> W = f29_mul<F>(U, V);
+  F29<F> S = f29_mul<F>(a.x, V);
+  F29<F> xx = f29_sqr<F>(a.x);
+  F29<F> M = f29_add<F>(f29_add<F>(xx, xx), xx);        // < 6m
+  F29<F> X3 = f29_sub<F>(f29_sqr<F>(M), f29_add<F>(S, S), F::P4);  // < 6m
+  F29<F> Y3 = f29_sub<F>(f29_mul<F>(M, f29_sub<F>(S, X3, F::P8)), f29_mul<F>(W, a.y), F::P2);  // < 4m
   r.X = X3;
+  r.Y = Y3;
   r.ZZ = V;
   r.ZZZ = W;
   return r;
 }
 
-// doubling (dbl-2008-s-1, a = 0)
+// doubling (dbl-2008-s-1, a = 0); no 2-torsion in the prime-order subgroup
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_dbl_impl(const Xyzz<C>& p) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   if (xyzz_is_inf<C>(p)) return p;
   Xyzz<C> r;
-  Fe<F> U = fe_dbl<F>(p.Y);
-  Fe<F> V = fe_sqr<F>(U);
-  Fe<F> W = fe_mul<F>(U, V);
-  Fe<F> S = fe_mul<F>(p.X, V);
-  Fe<F> xx = fe_sqr<F>(p.X);
-  Fe<F> M = fe_add<F>(fe_dbl<F>(xx), xx);
-  Fe<F> X3 = fe_sub<F>(fe_sqr<F>(M), fe_dbl<F>(S));
-  r.Y = fe_sub<F>(fe_mul<F>(M, fe_sub<F>(S, X3)), fe_mul<F>(W, p.Y));
+  F29<F> U = f29_add<F>(p.Y, p.Y);                      // < 8m
+  F29<F> V = f29_sqr<F>(U);                             // < 2m (64 m^2)
+  F29<F> W = f29_mul<F>(U, V);
+  F29<F> S = f29_mul<F>(p.X, V);
+  F29<F> xx = f29_sqr<F>(p.X);
+  F29<F> M = f29_add<F>(f29_add<F>(xx, xx), xx);        // < 6m
+  F29<F> X3 = f29_sub<F>(f29_sqr<F>(M), f29_add<F>(S, S), F::P4);  // < 6m
+  F29<F> Y3 = f29_sub<F>(f29_mul<F>(M, f29_sub<F>(S, X3, F::P8)), f29_mul<F>(W, p.Y), F::P2);
   r.X = X3;
-  r.ZZ = fe_mul<F>(V, p.ZZ);
-  r.ZZZ = fe_mul<F>(W, p.ZZZ);
+  r.Y = Y3;
+  r.ZZ = f29_mul<F>(V, p.ZZ);
+  r.ZZZ = f29_mul<F>(W, p.ZZZ);
   return r;
 }
 
-// p + a, a affine (madd-2008-s); a must not be infinity
+// p + a, a affine and finite (madd-2008-s)
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
-  Fe<F> U2 = fe_mul<F>(a.x, p.ZZ);
-  Fe<F> S2 = fe_mul<F>(a.y, p.ZZZ);
-  Fe<F> P = fe_sub<F>(U2, p.X);
-  Fe<F> R = fe_sub<F>(S2, p.Y);
-  if (fe_is_zero<F>(P)) {
-    if (fe_is_zero<F>(R)) return xyzz_dbl_affine<C>(a);
+  F29<F> U2 = f29_mul<F>(a.x, p.ZZ);                    // < 2m
+  F29<F> S2 = f29_mul<F>(a.y, p.ZZZ);                   // < 2m
+  F29<F> P = f29_sub<F>(U2, p.X, F::P8);                // < 10m
+  F29<F> R = f29_sub<F>(S2, p.Y, F::P4);                // < 6m
+  F29<F> PP = f29_sqr<F>(P);                            // < 2m
+  if (f29_is_zero_lt2m<F>(PP)) {                        // x equal: double or cancel
+    if (f29_is_zero<F>(R)) return xyzz_dbl_affine<C>(a);
     return xyzz_inf<C>();
   }
-  Fe<F> PP = fe_sqr<F>(P);
-  Fe<F> PPP = fe_mul<F>(P, PP);
-  Fe<F> Q = fe_mul<F>(p.X, PP);
+  F29<F> PPP = f29_mul<F>(P, PP);
+  F29<F> Q = f29_mul<F>(p.X, PP);
   Xyzz<C> r;
-  r.X = fe_sub<F>(fe_sub<F>(fe_sqr<F>(R), PPP), fe_dbl<F>(Q));
-  r.Y = fe_sub<F>(fe_mul<F>(R, fe_sub<F>(Q, r.X)), fe_mul<F>(p.Y, PPP));
-  r.ZZ = fe_mul<F>(p.ZZ, PP);
-  r.ZZZ = fe_mul<F>(p.ZZZ, PPP);
+  r.X = f29_sub<F>(f29_sqr<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);       // < 8m
+  r.Y = f29_sub<F>(f29_mul<F>(R, f29_sub<F>(Q, r.X, F::P8)), f29_mul<F>(p.Y, PPP), F::P2);  // < 4m
+  r.ZZ = f29_mul<F>(p.ZZ, PP);
+  r.ZZZ = f29_mul<F>(p.ZZZ, PPP);
   return r;
 }
 
 // p + q (add-2008-s)
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_add_impl(const Xyzz<C>& p, const Xyzz<C>& q) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   if (xyzz_is_inf<C>(p)) return q;
   if (xyzz_is_inf<C>(q)) return p;
-  Fe<F> U1 = fe_mul<F>(p.X, q.ZZ);
-  Fe<F> U2 = fe_mul<F>(q.X, p.ZZ);
-  Fe<F> S1 = fe_mul<F>(p.Y, q.ZZZ);
-  Fe<F> S2 = fe_mul<F>(q.Y, p.ZZZ);
-  Fe<F> P = fe_sub<F>(U2, U1);
-  Fe<F> R = fe_sub<F>(S2, S1);
-  if (fe_is_zero<F>(P)) {
-    if (fe_is_zero<F>(R)) return xyzz_dbl<C>(p);
+  F29<F> U1 = f29_mul<F>(p.X, q.ZZ);
+  F29<F> U2 = f29_mul<F>(q.X, p.ZZ);
+  F29<F> S1 = f29_mul<F>(p.Y, q.ZZZ);
+  F29<F> S2 = f29_mul<F>(q.Y, p.ZZZ);
+  F29<F> P = f29_sub<F>(U2, U1, F::P2);                 // < 4m
+  F29<F> R = f29_sub<F>(S2, S1, F::P2);                 // < 4m
+  F29<F> PP = f29_sqr<F>(P);
+  if (f29_is_zero_lt2m<F>(PP)) {
+    if (f29_is_zero<F>(R)) return xyzz_dbl<C>(p);
     return xyzz_inf<C>();
   }
-  Fe<F> PP = fe_sqr<F>(P);
-  Fe<F> PPP = fe_mul<F>(P, PP);
-  Fe<F> Q = fe_mul<F>(U1, PP);
+  F29<F> PPP = f29_mul<F>(P, PP);
+  F29<F> Q = f29_mul<F>(U1, PP);
   Xyzz<C> r;
-  r.X = fe_sub<F>(fe_sub<F>(fe_sqr<F>(R), PPP), fe_dbl<F>(Q));
-  r.Y = fe_sub<F>(fe_mul<F>(R, fe_sub<F>(Q, r.X)), fe_mul<F>(S1, PPP));
-  r.ZZ = fe_mul<F>(fe_mul<F>(p.ZZ, q.ZZ), PP);
-  r.ZZZ = fe_mul<F>(fe_mul<F>(p.ZZZ, q.ZZZ), PPP);
+  r.X = f29_sub<F>(f29_sqr<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);
+  r.Y = f29_sub<F>(f29_mul<F>(R, f29_sub<F>(Q, r.X, F::P8)), f29_mul<F>(S1, PPP), F::P2);
+  r.ZZ = f29_mul<F>(f29_mul<F>(p.ZZ, q.ZZ), PP);
+  r.ZZZ = f29_mul<F>(f29_mul<F>(p.ZZZ, q.ZZZ), PPP);
   return r;
+}
+
+// XYZZ -> affine, canonical Montgomery (< m).  Returns false for infinity.
+template <class C>
+KZGX_DEV bool xyzz_to_affine_impl(const Xyzz<C>& p, Affine<C>& out) {
+  using F = typename C::Fp29;
+  if (xyzz_is_inf<C>(p)) {
+    out.x = f29_zero<F>();
+    out.y = f29_zero<F>();
+    return false;
+  }
+  F29<F> t = f29_mul<F>(p.ZZ, p.ZZZ);
+  F29<F> i = f29_inv<F, C::Fp::N>(t, C::Fp::PM2);  // 1 / (ZZ ZZZ)
+  F29<F> izz = f29_mul<F>(i, p.ZZZ);               // 1 / ZZ
+  F29<F> izzz = f29_mul<F>(i, p.ZZ);               // 1 / ZZZ
+  out.x = f29_reduce<F>(f29_mul<F>(p.X, izz));
+  out.y = f29_reduce<F>(f29_mul<F>(p.Y, izzz));
+  return true;
 }
 
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_neg(const Xyzz<C>& p) {
+  using F = typename C::Fp29;
   Xyzz<C> r = p;
-  r.Y = fe_neg<typename C::Fp>(p.Y);
+  r.Y = f29_sub<F>(f29_zero<F>(), p.Y, F::P4);
   return r;
 }
 
-// k * p for a small non-negative integer k (double-and-add, MSB first)
 template <class C>
-KZGX_PT Xyzz<C> xyzz_mul_small(const Xyzz<C>& p, uint32_t k) {
-  Xyzz<C> acc = xyzz_inf<C>();
-  for (int b = 31; b >= 0; b--) {
-    acc = xyzz_dbl<C>(acc);
-    if ((k >> b) & 1u) acc = xyzz_add<C>(acc, p);
-  }
-  return acc;
-}
-
-// XYZZ -> affine (Montgomery).  Returns false for infinity.
-template <class C>
-KZGX_DEV bool xyzz_to_affine_impl(const Xyzz<C>& p, Affine<C>& out) {
-  using F = typename C::Fp;
-  if (xyzz_is_inf<C>(p)) {
-    out.x = fe_zero<F>();
-    out.y = fe_zero<F>();
-    return false;
-  }
-  Fe<F> t = fe_mul<F>(p.ZZ, p.ZZZ);
-  Fe<F> i = fe_inv<F>(t);           // 1 / (ZZ ZZZ)
-  Fe<F> izz = fe_mul<F>(i, p.ZZZ);   // 1 / ZZ
-  Fe<F> izzz = fe_mul<F>(i, p.ZZ);   // 1 / ZZZ
-  out.x = fe_mul<F>(p.X, izz);
-  out.y = fe_mul<F>(p.Y, izzz);
-  return true;
+KZGX_DEV Affine<C> affine_neg(const Affine<C>& a) {
+  using F = typename C::Fp29;
+  Affine<C> r = a;
+  r.y = f29_sub<F>(f29_zero<F>(), a.y, F::P);  // m - y, in (0, m]
+  return r;
 }
 
 // non-inlined entry points (cold paths and non-critical kernels)
@@ -223,41 +233,119 @@ KZGX_PT bool xyzz_to_affine(const Xyzz<C>& p, Affine<C>& out) {
   return xyzz_to_affine_impl<C>(p, out);
 }
 
-// point <-> 32-bit word arrays (Montgomery affine: x || y, 2N words)
+// ---- storage ---------------------------------------------------------------
+// table / workspace affine point: x (L words) || y (L words), padded to
+// affine_words<C>() so every point starts 16-byte aligned
 template <class C>
 KZGX_DEV Affine<C> affine_load(const uint32_t* p) {
-  using F = typename C::Fp;
+  constexpr int L = C::Fp29::L;
+  constexpr int AW = affine_words<C>();
+  uint32_t w[AW];
+#pragma unroll
+  for (int i = 0; i < AW / 4; i++) {
+    uint4 q = reinterpret_cast<const uint4*>(p)[i];
+    w[4 * i] = q.x;
+    w[4 * i + 1] = q.y;
+    w[4 * i + 2] = q.z;
+    w[4 * i + 3] = q.w;
+  }
   Affine<C> a;
-  a.x = fe_load<F>(p);
-  a.y = fe_load<F>(p + F::N);
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    a.x.v[i] = w[i];
+    a.y.v[i] = w[L + i];
+  }
   return a;
 }
 
 template <class C>
 KZGX_DEV void affine_store(uint32_t* p, const Affine<C>& a) {
-  using F = typename C::Fp;
-  fe_store<F>(p, a.x);
-  fe_store<F>(p + F::N, a.y);
+  constexpr int L = C::Fp29::L;
+  constexpr int AW = affine_words<C>();
+  uint32_t w[AW];
+#pragma unroll
+  for (int i = 0; i < AW; i++) w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    w[i] = a.x.v[i];
+    w[L + i] = a.y.v[i];
+  }
+#pragma unroll
+  for (int i = 0; i < AW / 4; i++)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_load(const uint32_t* p) {
-  using F = typename C::Fp;
+  constexpr int L = C::Fp29::L;
+  uint32_t w[4 * L];
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    uint4 q = reinterpret_cast<const uint4*>(p)[i];
+    w[4 * i] = q.x;
+    w[4 * i + 1] = q.y;
+    w[4 * i + 2] = q.z;
+    w[4 * i + 3] = q.w;
+  }
   Xyzz<C> r;
-  r.X = fe_load<F>(p);
-  r.Y = fe_load<F>(p + F::N);
-  r.ZZ = fe_load<F>(p + 2 * F::N);
-  r.ZZZ = fe_load<F>(p + 3 * F::N);
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    r.X.v[i] = w[i];
+    r.Y.v[i] = w[L + i];
+    r.ZZ.v[i] = w[2 * L + i];
+    r.ZZZ.v[i] = w[3 * L + i];
+  }
   return r;
 }
 
 template <class C>
 KZGX_DEV void xyzz_store(uint32_t* p, const Xyzz<C>& a) {
-  using F = typename C::Fp;
-  fe_store<F>(p, a.X);
-  fe_store<F>(p + F::N, a.Y);
-  fe_store<F>(p + 2 * F::N, a.ZZ);
-  fe_store<F>(p + 3 * F::N, a.ZZZ);
+  constexpr int L = C::Fp29::L;
+  uint32_t w[4 * L];
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    w[i] = a.X.v[i];
+    w[L + i] = a.Y.v[i];
+    w[2 * L + i] = a.ZZ.v[i];
+    w[3 * L + i] = a.ZZZ.v[i];
+  }
+#pragma unroll
+  for (int i = 0; i < L; i++)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// canonical little-endian 32-bit-word affine point (x || y, N words each;
+// all-zero = infinity) <-> radix-2^29 Montgomery.  Returns false for infinity.
+template <class C>
+KZGX_DEV bool affine_from_canonical(const uint32_t* p, Affine<C>& a) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    wx[i] = p[i];
+    wy[i] = p[N + i];
+    o |= wx[i] | wy[i];
+  }
+  a.x = f29_reduce<F>(f29_to_mont<F>(f29_from_words<F, N>(wx)));
+  a.y = f29_reduce<F>(f29_to_mont<F>(f29_from_words<F, N>(wy)));
+  return o != 0;
+}
+
+// affine (Montgomery, < m) -> canonical words; infinity writes zeros
+template <class C>
+KZGX_DEV void affine_to_canonical(uint32_t* p, const Affine<C>& a, bool finite) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  f29_to_words<F, N>(f29_from_mont<F>(a.x), wx);
+  f29_to_words<F, N>(f29_from_mont<F>(a.y), wy);
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    p[i] = finite ? wx[i] : 0u;
+    p[N + i] = finite ? wy[i] : 0u;
+  }
 }
 
 }  // namespace kzgx

@@ -1,0 +1,276 @@
+// Base-field (Fp) arithmetic for the G1 hot path on gfx950: radix-2^29
+// Montgomery with lazy reduction.
+//
+// Why radix 2^29 (measured, scripts/micro_valu.hip, profiles/r01_micro_valu.txt):
+// on gfx950 v_mad_u64_u32 issues at about the cost of any other 64-bit /
+// carry-out VALU op (~4.5-5 SIMD cycles per wave-instruction), so the cost of
+// a 32-bit-limb CIOS product is dominated by the carry glue around each mad
+// (v_lshl_add_u64 + v_mov pairs: ~600 instructions per product).  With 29-bit
+// limbs every partial product fits a single v_mad_u64_u32 that accumulates
+// into a 64-bit column sum with >= 2 bits of headroom per column (product
+// scanning / FIPS), so a product is one mad per partial product plus a shift
+// and a mask per column: 1.6x faster per multiplication.
+//
+// Lazy reduction: R = 2^(29 L) >= 64 m (BN254: L = 9, R/m ~ 222; BLS12-381:
+// L = 14), so a Montgomery product of inputs a, b with a b < (R/m) m^2 comes
+// out < 2m with no final subtraction.  Additions and subtractions are plain
+// carry-propagated limb arithmetic with a multiple of m added to keep
+// subtractions non-negative; curve.hpp documents the bound of every value.
+// Only equality tests and the final output need a full reduction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "curve_consts.h"
+
+#ifndef KZGX_DEV
+#define KZGX_DEV __device__ __forceinline__
+#endif
+
+namespace kzgx {
+
+constexpr uint32_t M29 = (1u << 29) - 1;
+
+template <class F>
+struct F29 {
+  uint32_t v[F::L];
+};
+
+template <class F>
+KZGX_DEV F29<F> f29_const(const uint32_t (&c)[F::L]) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = c[i];
+  return r;
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_zero() {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = 0;
+  return r;
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_one() {
+  return f29_const<F>(F::ONE);
+}
+
+template <class F>
+KZGX_DEV bool f29_is_zero_exact(const F29<F>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) o |= a.v[i];
+  return o == 0;
+}
+
+// a + b, carry propagated (no modular reduction; caller tracks the bound)
+template <class F>
+KZGX_DEV F29<F> f29_add(const F29<F>& a, const F29<F>& b) {
+  F29<F> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & M29;
+    c = s >> 29;
+  }
+  return r;
+}
+
+// a + K - b where K = k m >= b (so the result is non-negative)
+template <class F>
+KZGX_DEV F29<F> f29_sub(const F29<F>& a, const F29<F>& b, const uint32_t (&K)[F::L]) {
+  F29<F> r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    int32_t s = (int32_t)(a.v[i] + K[i]) - (int32_t)b.v[i] + c;
+    r.v[i] = (uint32_t)s & M29;
+    c = s >> 29;  // arithmetic shift: -1, 0 or 1
+  }
+  return r;
+}
+
+// Montgomery product a b / R mod m, product scanning; output < 2m when
+// a b < (R / m) m^2 (see header).
+template <class F>
+KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
+  constexpr int L = F::L;
+  uint32_t q[L];
+  F29<F> t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) acc += (uint64_t)a.v[i] * b.v[j];
+    }
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+    }
+    if (k < L) {
+      q[k] = ((uint32_t)acc * F::INV) & M29;
+      acc += (uint64_t)q[k] * F::P[0];
+    } else {
+      t.v[k - L] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+  }
+  t.v[L - 1] = (uint32_t)acc;
+  return t;
+}
+
+// Montgomery square: cross products once, against a doubled operand
+template <class F>
+KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {
+  constexpr int L = F::L;
+  uint32_t q[L], d[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) d[i] = a.v[i] << 1;
+  F29<F> t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j > i && j < L) acc += (uint64_t)a.v[i] * d[j];
+    }
+    if ((k & 1) == 0 && (k >> 1) < L) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+    }
+    if (k < L) {
+      q[k] = ((uint32_t)acc * F::INV) & M29;
+      acc += (uint64_t)q[k] * F::P[0];
+    } else {
+      t.v[k - L] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+  }
+  t.v[L - 1] = (uint32_t)acc;
+  return t;
+}
+
+// a - K if a >= K (K a multiple of m)
+template <class F>
+KZGX_DEV F29<F> f29_csub(const F29<F>& a, const uint32_t (&K)[F::L]) {
+  F29<F> r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    int32_t s = (int32_t)a.v[i] - (int32_t)K[i] + c;
+    r.v[i] = (uint32_t)s & M29;
+    c = s >> 29;
+  }
+  const bool keep = c < 0;  // borrow out: a < K
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = keep ? a.v[i] : r.v[i];
+  return r;
+}
+
+// full reduction of a < 16 m to [0, m)
+template <class F>
+KZGX_DEV F29<F> f29_reduce(const F29<F>& a) {
+  F29<F> r = f29_csub<F>(a, F::P8);
+  r = f29_csub<F>(r, F::P4);
+  r = f29_csub<F>(r, F::P2);
+  return f29_csub<F>(r, F::P);
+}
+
+// a == 0 mod m for a < 2m, with a one-limb filter in front of the full test
+template <class F>
+KZGX_DEV bool f29_is_zero_lt2m(const F29<F>& a) {
+  const uint32_t v0 = a.v[0];
+  if (v0 != 0u && v0 != F::LOW[1]) return false;
+  return f29_is_zero_exact<F>(f29_csub<F>(a, F::P));
+}
+
+template <class F>
+KZGX_DEV bool f29_is_zero(const F29<F>& a) {
+  return f29_is_zero_exact<F>(f29_reduce<F>(a));
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_to_mont(const F29<F>& a) {
+  return f29_mul<F>(a, f29_const<F>(F::R2));
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_from_mont(const F29<F>& a) {
+  F29<F> one = f29_zero<F>();
+  one.v[0] = 1;
+  return f29_reduce<F>(f29_mul<F>(a, one));
+}
+
+// canonical little-endian 32-bit words (NW of them) <-> radix-2^29 limbs
+template <class F, int NW>
+KZGX_DEV F29<F> f29_from_words(const uint32_t (&w)[NW]) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int bit = 29 * i, wd = bit >> 5, sh = bit & 31;
+    uint32_t lo = wd < NW ? w[wd] : 0u;
+    uint32_t hi = wd + 1 < NW ? w[wd + 1] : 0u;
+    r.v[i] = (sh == 0 ? lo : __builtin_amdgcn_alignbit(hi, lo, sh)) & M29;
+  }
+  return r;
+}
+
+template <class F, int NW>
+KZGX_DEV void f29_to_words(const F29<F>& a, uint32_t (&w)[NW]) {
+#pragma unroll
+  for (int j = 0; j < NW; j++) {
+    const int bit = 32 * j, li = bit / 29, sh = bit % 29;
+    uint64_t v = li < F::L ? (uint64_t)(a.v[li] >> sh) : 0u;
+    int have = 29 - sh;
+    if (li + 1 < F::L) v |= (uint64_t)a.v[li + 1] << have;
+    if (li + 2 < F::L && have + 29 < 32) v |= (uint64_t)a.v[li + 2] << (have + 29);
+    w[j] = (uint32_t)v;
+  }
+}
+
+// a^(m-2), 4-bit fixed window over the 32-bit exponent words PM2 (NW words)
+template <class F, int NW>
+__device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW]) {
+  F29<F> tbl[16];
+  tbl[0] = f29_one<F>();
+  tbl[1] = a;
+#pragma unroll
+  for (int i = 2; i < 16; i++) tbl[i] = f29_mul<F>(tbl[i - 1], a);
+  F29<F> acc = f29_one<F>();
+  for (int nib = 8 * NW - 1; nib >= 0; nib--) {
+#pragma unroll
+    for (int s = 0; s < 4; s++) acc = f29_sqr<F>(acc);
+    const uint32_t d = (pm2[nib >> 3] >> (4 * (nib & 7))) & 15u;
+    F29<F> m = tbl[0];
+#pragma unroll
+    for (int k = 1; k < 16; k++)
+      if (k == (int)d) m = tbl[k];
+    acc = f29_mul<F>(acc, m);
+  }
+  return acc;
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_load(const uint32_t* p) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = p[i];
+  return r;
+}
+
+template <class F>
+KZGX_DEV void f29_store(uint32_t* p, const F29<F>& a) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) p[i] = a.v[i];
+}
+
+}  // namespace kzgx

@@ -122,6 +122,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->c.device);
   (void)hipStreamSynchronize(ctx->c.stream);
+  (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_inf, c.ws.counts, c.ws.offsets, c.ws.cursors, c.ws.entries, c.ws.bsum,
                   c.ws.heads, c.ws.tails, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
@@ -135,6 +136,50 @@ void kzgx_destroy(kzgx_ctx* ctx) {
 int kzgx_sync(kzgx_ctx* ctx) {
   KZGX_TRY(activate(ctx));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+void* kzgx_stream(kzgx_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
+
+int kzgx_prof_enable(kzgx_ctx* ctx, int on) {
+  KZGX_TRY(activate(ctx));
+  ctx->c.prof_on = on != 0;
+  return KZGX_OK;
+}
+
+int kzgx_prof_read(kzgx_ctx* ctx, const char* name, double* total_ms, int* count) {
+  KZGX_TRY(activate(ctx));
+  if (!name || !total_ms || !count) return KZGX_ERR_ARG;
+  double tot = 0;
+  int cnt = 0;
+  std::vector<kzgx::ProfRec> keep;
+  for (auto& r : ctx->c.prof) {
+    if (std::strcmp(r.name, name) != 0) {
+      keep.push_back(r);
+      continue;
+    }
+    KZGX_TRY_HIP(hipEventSynchronize(r.b));
+    float ms = 0;
+    KZGX_TRY_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    tot += ms;
+    cnt++;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  ctx->c.prof.swap(keep);
+  *total_ms = tot;
+  *count = cnt;
+  return KZGX_OK;
+}
+
+int kzgx_prof_clear(kzgx_ctx* ctx) {
+  KZGX_TRY(activate(ctx));
+  for (auto& r : ctx->c.prof) {
+    (void)hipEventSynchronize(r.b);
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  ctx->c.prof.clear();
   return KZGX_OK;
 }
 

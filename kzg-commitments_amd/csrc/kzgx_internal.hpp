@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/kzg_gpu.h"
 
 #ifndef KZGX_WINDOW_BITS
@@ -32,6 +34,12 @@ struct MsmWs {
   size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0;
 };
 
+// optional per-kernel timing with HIP events on the launch stream
+struct ProfRec {
+  const char* name;
+  hipEvent_t a, b;
+};
+
 struct Ctx {
   int curve = 0;
   int device = 0;
@@ -45,12 +53,34 @@ struct Ctx {
   uint8_t* d_inf = nullptr;  // [n_srs]
   size_t inf_bytes = 0;
   MsmWs ws;
+  bool prof_on = false;
+  std::vector<ProfRec> prof;
   void* d_poly_ws = nullptr;  // scratch for the Fr polynomial kernels
   size_t poly_ws_b = 0;
   // staging for host-pointer entry points
   void* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_b[4] = {0, 0, 0, 0};
   int base_words() const { return curve == KZGX_CURVE_BN254 ? 8 : 12; }
+};
+
+// bracket one launch with events when profiling is enabled
+struct ProfScope {
+  Ctx* ctx;
+  hipStream_t st;
+  ProfRec rec;
+  ProfScope(Ctx* c, hipStream_t s, const char* name) : ctx(c), st(s) {
+    rec.name = nullptr;
+    if (!ctx->prof_on) return;
+    rec.name = name;
+    (void)hipEventCreate(&rec.a);
+    (void)hipEventCreate(&rec.b);
+    (void)hipEventRecord(rec.a, st);
+  }
+  ~ProfScope() {
+    if (!rec.name) return;
+    (void)hipEventRecord(rec.b, st);
+    ctx->prof.push_back(rec);
+  }
 };
 
 // grow-only device allocation (frees the old block)

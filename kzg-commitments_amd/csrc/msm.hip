@@ -33,36 +33,34 @@ namespace kzgx {
 template <class C>
 __global__ void k_srs_to_mont(const uint32_t* __restrict__ canon, uint32_t* __restrict__ table, uint8_t* __restrict__ inf,
                               uint32_t n) {
-  using F = typename C::Fp;
+  constexpr int AW = affine_words<C>();
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Affine<C> a = affine_load<C>(canon + (size_t)i * 2 * F::N);
-  bool is_inf = fe_is_zero<F>(a.x) && fe_is_zero<F>(a.y);
-  inf[i] = is_inf ? 1 : 0;
-  a.x = fe_to_mont<F>(a.x);
-  a.y = fe_to_mont<F>(a.y);
-  affine_store<C>(table + (size_t)i * 2 * F::N, a);
+  Affine<C> a;
+  const bool finite = affine_from_canonical<C>(canon + (size_t)i * 2 * C::Fp::N, a);
+  inf[i] = finite ? 0 : 1;
+  affine_store<C>(table + (size_t)i * AW, a);
 }
 
 // T[w][i] = 2^c T[w-1][i] for w = 1..W-1
 template <class C>
 __global__ void k_table_build(uint32_t* __restrict__ table, const uint8_t* __restrict__ inf, uint32_t n, int W, int c) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
+  constexpr int AW = affine_words<C>();
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const size_t PW = 2 * F::N;
-  Affine<C> a = affine_load<C>(table + (size_t)i * PW);
+  Affine<C> a = affine_load<C>(table + (size_t)i * AW);
   const bool is_inf = inf[i] != 0;
   for (int w = 1; w < W; w++) {
     if (!is_inf) {
       Xyzz<C> p = xyzz_from_affine<C>(a);
       for (int s = 0; s < c; s++) p = xyzz_dbl<C>(p);
       if (!xyzz_to_affine<C>(p, a)) {
-        a.x = fe_zero<F>();
-        a.y = fe_zero<F>();
+        a.x = f29_zero<F>();
+        a.y = f29_zero<F>();
       }
     }
-    affine_store<C>(table + ((size_t)w * n + i) * PW, a);
+    affine_store<C>(table + ((size_t)w * n + i) * AW, a);
   }
 }
 
@@ -214,9 +212,8 @@ __global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ table, uint32_t K, size_t smax,
                                                    uint32_t* __restrict__ bsum, uint32_t* __restrict__ heads,
                                                    uint32_t* __restrict__ tails) {
-  using F = typename C::Fp;
-  constexpr int PW = 2 * F::N;
-  constexpr int XW = 4 * F::N;
+  constexpr int PW = affine_words<C>();
+  constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t* off = offsets + (size_t)b * (nb + 1);
@@ -252,7 +249,7 @@ __global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ 
     }
     const uint32_t e = ent[p];
     Affine<C> a = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
-    if (e >> 31) a.y = fe_neg<F>(a.y);
+    if (e >> 31) a = affine_neg<C>(a);
     acc = xyzz_add_affine_impl<C>(acc, a);
   }
   uint32_t* dst;
@@ -272,8 +269,7 @@ __global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ heads,
                                                     const uint32_t* __restrict__ tails, uint32_t* __restrict__ out,
                                                     uint32_t* __restrict__ out_inf) {
-  using F = typename C::Fp;
-  constexpr int XW = 4 * F::N;
+  constexpr int XW = xyzz_words<C>();
   extern __shared__ uint32_t lds[];  // 256 points, XW words each
   const uint32_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
@@ -326,11 +322,7 @@ __global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__
   if (t == 0) {
     Affine<C> a;
     bool fin = xyzz_to_affine<C>(sum, a);
-    if (fin) {
-      a.x = fe_from_mont<F>(a.x);
-      a.y = fe_from_mont<F>(a.y);
-    }
-    affine_store<C>(out + (size_t)b * 2 * F::N, a);
+    affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
     out_inf[b] = fin ? 0u : 1u;
   }
 }
@@ -340,9 +332,8 @@ __global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__
 // --------------------------------------------------------------------------
 template <class C>
 int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
-  using F = typename C::Fp;
   const int W = ctx->W;
-  const size_t pw = 2 * F::N * sizeof(uint32_t);
+  const size_t pw = affine_words<C>() * sizeof(uint32_t);
   KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table, (size_t)W * n * pw, &ctx->table_bytes));
   KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_inf, n, &ctx->inf_bytes));
   dim3 blk(256), grd((unsigned)((n + 255) / 256));
@@ -356,13 +347,12 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
 template <class C, int CB>
 int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
                    uint32_t* d_out_inf, hipStream_t st) {
-  using F = typename C::Fp;
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   const uint32_t K = ctx->seg_k;
   const size_t emax = (size_t)n * W;
   const size_t smax = (emax + K - 1) / K;
-  const size_t XB = 4 * F::N * sizeof(uint32_t);
+  const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
   MsmWs& ws = ctx->ws;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, batch * NB * 4, &ws.counts_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, batch * (NB + 1) * 4, &ws.offsets_b));
@@ -374,15 +364,30 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   KZGX_TRY_HIP(hipMemsetAsync(ws.counts, 0, batch * NB * 4, st));
   dim3 blk(256);
   dim3 gs((unsigned)((n + 255) / 256), (unsigned)batch);
-  hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts);
-  hipLaunchKernelGGL(k_msm_scan, dim3((unsigned)batch), blk, 0, st, ws.counts, ws.offsets, ws.cursors, NB);
-  hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.cursors,
-                     ws.entries, emax, (uint32_t)ctx->n_srs);
-  dim3 ga((unsigned)((smax + 255) / 256), (unsigned)batch);
-  hipLaunchKernelGGL(k_msm_accum<C>, ga, blk, 0, st, ws.entries, emax, ws.offsets, NB, ctx->d_table, K, smax, ws.bsum,
-                     ws.heads, ws.tails);
-  hipLaunchKernelGGL(k_msm_reduce<C>, dim3((unsigned)batch), blk, 256 * XB, st, ws.offsets, NB, K, smax, ws.bsum,
-                     ws.heads, ws.tails, d_out, d_out_inf);
+  {
+    ProfScope p(ctx, st, "msm_count");
+    hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts);
+  }
+  {
+    ProfScope p(ctx, st, "msm_scan");
+    hipLaunchKernelGGL(k_msm_scan, dim3((unsigned)batch), blk, 0, st, ws.counts, ws.offsets, ws.cursors, NB);
+  }
+  {
+    ProfScope p(ctx, st, "msm_scatter");
+    hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
+                       ws.cursors, ws.entries, emax, (uint32_t)ctx->n_srs);
+  }
+  {
+    ProfScope p(ctx, st, "msm_accum");
+    dim3 ga((unsigned)((smax + 255) / 256), (unsigned)batch);
+    hipLaunchKernelGGL(k_msm_accum<C>, ga, blk, 0, st, ws.entries, emax, ws.offsets, NB, ctx->d_table, K, smax,
+                       ws.bsum, ws.heads, ws.tails);
+  }
+  {
+    ProfScope p(ctx, st, "msm_reduce");
+    hipLaunchKernelGGL(k_msm_reduce<C>, dim3((unsigned)batch), blk, 256 * XB, st, ws.offsets, NB, K, smax, ws.bsum,
+                       ws.heads, ws.tails, d_out, d_out_inf);
+  }
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }

@@ -266,9 +266,10 @@ __global__ __launch_bounds__(256) void k_interp_coeffs(const uint32_t* __restric
 // host side
 // --------------------------------------------------------------------------
 template <class FR>
-static int quotient_single_impl(const uint32_t* d_coeffs, size_t n, size_t cstride, const uint32_t* d_z, size_t batch,
+static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, size_t cstride, const uint32_t* d_z, size_t batch,
                                 uint32_t* d_q, size_t qstride, uint32_t* d_y, hipStream_t st) {
   if (batch == 0) return KZGX_OK;
+  ProfScope prof(ctx, st, "quotient_single");
   hipLaunchKernelGGL(k_quotient_single<FR>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, d_coeffs,
                      (uint32_t)n, cstride, d_z, (uint32_t)batch, d_q, qstride, d_y);
   KZGX_TRY_HIP(hipGetLastError());
@@ -278,8 +279,8 @@ static int quotient_single_impl(const uint32_t* d_coeffs, size_t n, size_t cstri
 int quotient_single(Ctx* ctx, const uint32_t* d_coeffs, size_t n, size_t coeff_stride_words, const uint32_t* d_z,
                     size_t batch, uint32_t* d_q, size_t q_stride_words, uint32_t* d_y, hipStream_t st) {
   return ctx->curve == KZGX_CURVE_BN254
-             ? quotient_single_impl<BN254Fr>(d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y, st)
-             : quotient_single_impl<BLS12381Fr>(d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y,
+             ? quotient_single_impl<BN254Fr>(ctx, d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y, st)
+             : quotient_single_impl<BLS12381Fr>(ctx, d_coeffs, n, coeff_stride_words, d_z, batch, d_q, q_stride_words, d_y,
                                                 st);
 }
 

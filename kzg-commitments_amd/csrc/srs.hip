@@ -16,7 +16,7 @@ namespace kzgx {
 template <class C>
 __global__ __launch_bounds__(256) void k_gen_srs(const uint32_t* __restrict__ tau_canon, uint64_t start, uint32_t n,
                                                  uint32_t* __restrict__ out) {
-  using F = typename C::Fp;
+  using F = typename C::Fp29;
   using FR = typename C::Fr;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -30,42 +30,33 @@ __global__ __launch_bounds__(256) void k_gen_srs(const uint32_t* __restrict__ ta
   }
   e = fe_from_mont<FR>(e);
   Affine<C> g;
-  g.x = fe_const<F>(C::GX);
-  g.y = fe_const<F>(C::GY);
+  g.x = f29_const<F>(C::GX29);
+  g.y = f29_const<F>(C::GY29);
   Xyzz<C> acc = xyzz_inf<C>();
   for (int b = 8 * FR::N * 4 - 1; b >= 0; b--) {
     acc = xyzz_dbl<C>(acc);
     if ((e.v[b >> 5] >> (b & 31)) & 1u) acc = xyzz_add_affine<C>(acc, g);
   }
   Affine<C> a;
-  if (xyzz_to_affine<C>(acc, a)) {
-    a.x = fe_from_mont<F>(a.x);
-    a.y = fe_from_mont<F>(a.y);
-  }
-  affine_store<C>(out + (size_t)i * 2 * F::N, a);
+  const bool fin = xyzz_to_affine<C>(acc, a);
+  affine_to_canonical<C>(out + (size_t)i * 2 * C::Fp::N, a, fin);
 }
 
 // out = sum of count canonical affine points (zero or flagged = infinity)
 template <class C>
 __global__ void k_g1_sum(const uint32_t* __restrict__ xy, const uint32_t* __restrict__ inf, uint32_t count,
                          uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
-  using F = typename C::Fp;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Xyzz<C> acc = xyzz_inf<C>();
   for (uint32_t i = 0; i < count; i++) {
-    Affine<C> a = affine_load<C>(xy + (size_t)i * 2 * F::N);
-    if ((inf && inf[i]) || (fe_is_zero<F>(a.x) && fe_is_zero<F>(a.y))) continue;
-    a.x = fe_to_mont<F>(a.x);
-    a.y = fe_to_mont<F>(a.y);
+    Affine<C> a;
+    const bool finite = affine_from_canonical<C>(xy + (size_t)i * 2 * C::Fp::N, a);
+    if ((inf && inf[i]) || !finite) continue;
     acc = xyzz_add_affine<C>(acc, a);
   }
   Affine<C> r;
   bool fin = xyzz_to_affine<C>(acc, r);
-  if (fin) {
-    r.x = fe_from_mont<F>(r.x);
-    r.y = fe_from_mont<F>(r.y);
-  }
-  affine_store<C>(out, r);
+  affine_to_canonical<C>(out, r, fin);
   *out_inf = fin ? 0u : 1u;
 }
 
