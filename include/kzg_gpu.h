@@ -76,6 +76,11 @@ int kzgx_prof_enable(kzgx_ctx* ctx, int on);
 int kzgx_prof_read(kzgx_ctx* ctx, const char* name, double* total_ms, int* count);
 int kzgx_prof_clear(kzgx_ctx* ctx);
 
+/* tuning: signed-digit window bits (10..13; default 12 or $KZGX_WINDOW_BITS),
+ * settable only before the SRS is loaded; entries per accumulation thread */
+int kzgx_set_window_bits(kzgx_ctx* ctx, int c);
+int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
+
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */
 int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n);

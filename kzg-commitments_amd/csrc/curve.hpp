@@ -133,7 +133,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
   F29<F> R = f29_sub<F>(S2, p.Y, F::P4);                // < 6m
   F29<F> PP = f29_sqr<F>(P);                            // < 2m
   if (f29_is_zero_lt2m<F>(PP)) {                        // x equal: double or cancel
-    if (f29_is_zero<F>(R)) return xyzz_dbl_affine<C>(a);
+    if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);  // inline: no call frame in the hot loop
     return xyzz_inf<C>();
   }
   F29<F> PPP = f29_mul<F>(P, PP);

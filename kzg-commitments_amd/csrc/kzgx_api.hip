@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -107,6 +108,10 @@ int kzgx_create(kzgx_ctx** out, int curve, int device) {
   if (!ctx) return KZGX_ERR_OOM;
   ctx->c.curve = curve;
   ctx->c.device = device;
+  if (const char* e = getenv("KZGX_WINDOW_BITS")) {
+    int c = atoi(e);
+    if (kzgx::window_bits_supported(c)) ctx->c.c = c;
+  }
   ctx->c.W = (257 + ctx->c.c - 1) / ctx->c.c;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking);
@@ -124,11 +129,15 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->c.stream);
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
-  void* bufs[] = {c.d_table, c.d_inf, c.ws.counts, c.ws.offsets, c.ws.cursors, c.ws.entries, c.ws.bsum,
-                  c.ws.heads, c.ws.tails, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
+  void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
                   c.d_poly_ws, ctx->d_srs_canon};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  for (auto& w : c.ws) {
+    void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum, w.heads, w.tails, w.rt, w.q};
+    for (void* p : wb)
+      if (p) (void)hipFree(p);
+  }
   (void)hipStreamDestroy(c.stream);
   delete ctx;
 }
@@ -180,6 +189,22 @@ int kzgx_prof_clear(kzgx_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   ctx->c.prof.clear();
+  return KZGX_OK;
+}
+
+int kzgx_set_window_bits(kzgx_ctx* ctx, int c) {
+  KZGX_TRY(activate(ctx));
+  if (!kzgx::window_bits_supported(c)) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs != 0) return KZGX_ERR_ARG;  // the fixed-base table depends on c
+  ctx->c.c = c;
+  ctx->c.W = (257 + c - 1) / c;
+  return KZGX_OK;
+}
+
+int kzgx_set_segment(kzgx_ctx* ctx, unsigned k) {
+  KZGX_TRY(activate(ctx));
+  if (k < 1 || k > 4096) return KZGX_ERR_ARG;
+  ctx->c.seg_k = k;
   return KZGX_OK;
 }
 
@@ -288,8 +313,13 @@ int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n
   const size_t nq = n > 0 ? n - 1 : 0;
   if (nq > ctx->c.n_srs) return KZGX_ERR_DEGREE;
   hipStream_t st = pick(ctx, stream);
+  kzgx::MsmWs* ws = ctx->c.ws_for(st);
+  if (!ws) return KZGX_ERR_ARG;
   void* d_q = nullptr;
-  if (nq) KZGX_TRY(stage(ctx, 3, nq * batch * 32, &d_q));
+  if (nq) {
+    KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ws->q, nq * batch * 32, &ws->q_b));
+    d_q = ws->q;
+  }
   KZGX_TRY(kzgx_quotient_single_batch_device(ctx, d_coeffs, n, coeff_stride, d_z, batch, d_q, nq, d_y, st));
   return kzgx_msm_g1_batch_device(ctx, d_q, nq, batch, nq, d_out_xy, d_out_is_inf, st);
 }

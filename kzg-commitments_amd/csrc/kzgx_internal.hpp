@@ -9,7 +9,7 @@
 #include "../../include/kzg_gpu.h"
 
 #ifndef KZGX_WINDOW_BITS
-#define KZGX_WINDOW_BITS 10
+#define KZGX_WINDOW_BITS 12  // default signed-digit window (10..13 supported)
 #endif
 
 #define KZGX_TRY(expr)                 \
@@ -30,9 +30,14 @@ int hip_fail(hipError_t e);
 
 struct MsmWs {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursors = nullptr, *entries = nullptr;
-  uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr;
-  size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0;
+  uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr, *rt = nullptr, *q = nullptr;
+  size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0, rt_b = 0,
+         q_b = 0;
+  hipStream_t owner = nullptr;  // workspaces are per stream so calls on
+  bool used = false;            // different streams may run concurrently
 };
+
+constexpr int KZGX_MAX_STREAMS = 8;
 
 // optional per-kernel timing with HIP events on the launch stream
 struct ProfRec {
@@ -46,13 +51,26 @@ struct Ctx {
   hipStream_t stream = nullptr;
   int c = KZGX_WINDOW_BITS;  // window bits
   int W = 0;                 // windows
-  uint32_t seg_k = 32;       // entries per accumulation thread
+  uint32_t seg_k = 128;      // entries per accumulation thread
   size_t n_srs = 0;
   uint32_t* d_table = nullptr;  // [W][n_srs] affine Montgomery points
   size_t table_bytes = 0;
   uint8_t* d_inf = nullptr;  // [n_srs]
   size_t inf_bytes = 0;
-  MsmWs ws;
+  MsmWs ws[KZGX_MAX_STREAMS];
+  // the workspace bound to stream st (claimed on first use); nullptr when
+  // more than KZGX_MAX_STREAMS distinct streams are used
+  MsmWs* ws_for(hipStream_t st) {
+    for (auto& w : ws)
+      if (w.used && w.owner == st) return &w;
+    for (auto& w : ws)
+      if (!w.used) {
+        w.used = true;
+        w.owner = st;
+        return &w;
+      }
+    return nullptr;
+  }
   bool prof_on = false;
   std::vector<ProfRec> prof;
   void* d_poly_ws = nullptr;  // scratch for the Fr polynomial kernels
@@ -86,6 +104,7 @@ struct ProfScope {
 // grow-only device allocation (frees the old block)
 int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap);
 
+bool window_bits_supported(int c);
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st);

@@ -262,22 +262,27 @@ __global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ 
   xyzz_store<C>(dst, acc);
 }
 
-// pass 5: finish buckets, sum_k (k+1) B_k, affine, canonical output
+// pass 5a: finish the buckets and their first-level weighted sums.
+// Thread t of MSM b owns buckets [t J, t J + J) (J = RED_J) and emits
+//   R_t = sum_j (j+1) B_{tJ+j}   and   T_t = sum_j B_{tJ+j}
+// so that sum_k (k+1) B_k = sum_t R_t + J sum_t t T_t.
+constexpr uint32_t RED_J = 8;
+
 template <class C>
-__global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
-                                                    size_t smax, const uint32_t* __restrict__ bsum,
-                                                    const uint32_t* __restrict__ heads,
-                                                    const uint32_t* __restrict__ tails, uint32_t* __restrict__ out,
-                                                    uint32_t* __restrict__ out_inf) {
+__global__ __launch_bounds__(256) void k_msm_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
+                                                         size_t smax, const uint32_t* __restrict__ bsum,
+                                                         const uint32_t* __restrict__ heads,
+                                                         const uint32_t* __restrict__ tails,
+                                                         uint32_t* __restrict__ rt) {
   constexpr int XW = xyzz_words<C>();
-  extern __shared__ uint32_t lds[];  // 256 points, XW words each
-  const uint32_t b = blockIdx.x;
-  const uint32_t t = threadIdx.x;
-  const uint32_t J = nb / 256;
+  const uint32_t b = blockIdx.y;
+  const uint32_t T1 = nb / RED_J;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T1) return;
   const uint32_t* off = offsets + (size_t)b * (nb + 1);
   Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
-  for (int j = (int)J - 1; j >= 0; j--) {
-    const uint32_t k = t * J + (uint32_t)j;
+  for (int j = (int)RED_J - 1; j >= 0; j--) {
+    const uint32_t k = t * RED_J + (uint32_t)j;
     const uint32_t o0 = off[k], o1 = off[k + 1];
     Xyzz<C> bk = xyzz_inf<C>();
     if (o1 > o0) {
@@ -286,42 +291,98 @@ __global__ __launch_bounds__(256) void k_msm_reduce(const uint32_t* __restrict__
         bk = xyzz_load<C>(bsum + ((size_t)b * nb + k) * XW);
       } else {
         bk = xyzz_load<C>(tails + ((size_t)b * smax + s0) * XW);
-        for (uint32_t s = s0 + 1; s <= s1; s++) bk = xyzz_add<C>(bk, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
+        for (uint32_t s = s0 + 1; s <= s1; s++) bk = xyzz_add_impl<C>(bk, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
       }
     }
-    run = xyzz_add<C>(run, bk);
-    sum = xyzz_add<C>(sum, run);
+    run = xyzz_add_impl<C>(run, bk);
+    sum = xyzz_add_impl<C>(sum, run);
   }
-  // suffix scan of run totals: S_t = sum_{u >= t} T_u
-  Xyzz<C> S = run;
-  xyzz_store<C>(lds + t * XW, S);
-  __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    Xyzz<C> o = xyzz_inf<C>();
-    if (t + d < 256) o = xyzz_load<C>(lds + (t + d) * XW);
-    __syncthreads();
-    S = xyzz_add<C>(S, o);
-    xyzz_store<C>(lds + t * XW, S);
-    __syncthreads();
+  uint32_t* dst = rt + ((size_t)b * T1 + t) * 2 * XW;
+  xyzz_store<C>(dst, sum);
+  xyzz_store<C>(dst + XW, run);
+}
+
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_shfl(const Xyzz<C>& p, int src) {
+  constexpr int L = C::Fp29::L;
+  Xyzz<C> r;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    r.X.v[i] = __shfl(p.X.v[i], src, 64);
+    r.Y.v[i] = __shfl(p.Y.v[i], src, 64);
+    r.ZZ.v[i] = __shfl(p.ZZ.v[i], src, 64);
+    r.ZZZ.v[i] = __shfl(p.ZZZ.v[i], src, 64);
   }
-  // V_t = R_t + J * S_t (t >= 1)
-  if (t >= 1) {
-    for (uint32_t m = J; m > 1; m >>= 1) S = xyzz_dbl<C>(S);
-    sum = xyzz_add<C>(sum, S);
-  }
-  xyzz_store<C>(lds + t * XW, sum);
-  __syncthreads();
-  for (uint32_t h = 128; h >= 1; h >>= 1) {
-    if (t < h) {
-      Xyzz<C> o = xyzz_load<C>(lds + (t + h) * XW);
-      sum = xyzz_add<C>(sum, o);
-      xyzz_store<C>(lds + t * XW, sum);
+  return r;
+}
+
+// pass 5b: one wavefront per MSM folds the T1 (R_t, T_t) pairs 4:1 per
+// level.  A level with scale s maps groups g = {4g..4g+3} to
+//   R'_g = sum_i R_{4g+i} + s (T_{4g+1} + 2 T_{4g+2} + 3 T_{4g+3}),
+//   T'_g = sum_i T_{4g+i},   scale' = 4 s,
+// which preserves  sum_t R_t + s sum_t t T_t.  When one pair is left, R is
+// the MSM value; lane 0 converts it to canonical affine.
+template <class C>
+__global__ __launch_bounds__(256) void k_msm_window_tail(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
+                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= batch) return;  // whole wavefront
+  const uint32_t* src = rt + (size_t)b * T1 * 2 * XW;
+  uint32_t cnt = T1;  // pairs alive
+  uint32_t s = RED_J;
+  // first level straight from memory: groups of G = max(4, T1/64) pairs so
+  // that at most 64 groups remain (T1 is a power of two in [64, 512])
+  Xyzz<C> R = xyzz_inf<C>(), T = xyzz_inf<C>();
+  {
+    const uint32_t G = T1 / 64 > 4 ? T1 / 64 : 4;
+    const uint32_t groups = cnt / G;
+    if (lane < groups) {
+      const uint32_t* g0 = src + (size_t)lane * G * 2 * XW;
+      Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>(), r = xyzz_inf<C>();
+      for (int i = (int)G - 1; i >= 1; i--) {
+        u = xyzz_add<C>(u, xyzz_load<C>(g0 + (size_t)i * 2 * XW + XW));
+        v = xyzz_add<C>(v, u);  // v = sum_i i T_i
+        r = xyzz_add<C>(r, xyzz_load<C>(g0 + (size_t)i * 2 * XW));
+      }
+      for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
+      r = xyzz_add<C>(r, xyzz_load<C>(g0));
+      R = xyzz_add<C>(r, v);
+      T = xyzz_add<C>(xyzz_load<C>(g0 + XW), u);
     }
-    __syncthreads();
+    cnt = groups;
+    s *= G;
   }
-  if (t == 0) {
+  // remaining levels inside the wavefront: lane g gathers lanes 4g..4g+3
+  while (cnt > 1) {
+    const uint32_t gsz = cnt >= 4 ? 4 : cnt;
+    const uint32_t groups = cnt / gsz;
+    Xyzz<C> r4[4], t4[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int from = (int)(lane * gsz + i) & 63;
+      r4[i] = xyzz_shfl<C>(R, from);
+      t4[i] = xyzz_shfl<C>(T, from);
+    }
+    if (lane < groups) {
+      Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>();
+      for (int i = (int)gsz - 1; i >= 1; i--) {
+        u = xyzz_add<C>(u, t4[i]);
+        v = xyzz_add<C>(v, u);
+      }
+      for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
+      Xyzz<C> r = r4[0];
+      for (uint32_t i = 1; i < gsz; i++) r = xyzz_add<C>(r, r4[i]);
+      R = xyzz_add<C>(r, v);
+      T = xyzz_add<C>(t4[0], u);
+    }
+    cnt = groups;
+    s *= gsz;
+  }
+  if (lane == 0) {
     Affine<C> a;
-    bool fin = xyzz_to_affine<C>(sum, a);
+    bool fin = xyzz_to_affine<C>(R, a);
     affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
     out_inf[b] = fin ? 0u : 1u;
   }
@@ -353,7 +414,9 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   const size_t emax = (size_t)n * W;
   const size_t smax = (emax + K - 1) / K;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
-  MsmWs& ws = ctx->ws;
+  MsmWs* wsp = ctx->ws_for(st);
+  if (!wsp) return KZGX_ERR_ARG;  // too many concurrent streams on one context
+  MsmWs& ws = *wsp;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, batch * NB * 4, &ws.counts_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, batch * (NB + 1) * 4, &ws.offsets_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, batch * NB * 4, &ws.cursors_b));
@@ -361,6 +424,7 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, batch * NB * XB, &ws.bsum_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, batch * smax * XB, &ws.heads_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, batch * smax * XB, &ws.tails_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / RED_J) * 2 * XB, &ws.rt_b));
   KZGX_TRY_HIP(hipMemsetAsync(ws.counts, 0, batch * NB * 4, st));
   dim3 blk(256);
   dim3 gs((unsigned)((n + 255) / 256), (unsigned)batch);
@@ -385,8 +449,11 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   }
   {
     ProfScope p(ctx, st, "msm_reduce");
-    hipLaunchKernelGGL(k_msm_reduce<C>, dim3((unsigned)batch), blk, 256 * XB, st, ws.offsets, NB, K, smax, ws.bsum,
-                       ws.heads, ws.tails, d_out, d_out_inf);
+    const uint32_t T1 = NB / RED_J;
+    hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB, K,
+                       smax, ws.bsum, ws.heads, ws.tails, ws.rt);
+    hipLaunchKernelGGL(k_msm_window_tail<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
+                       (uint32_t)batch, d_out, d_out_inf);
   }
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
@@ -397,13 +464,25 @@ int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
                                         : srs_upload_impl<BLS12381G1>(ctx, d_canon, n);
 }
 
+template <class C>
+static int msm_batch_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  switch (ctx->c) {
+    case 10: return msm_batch_impl<C, 10>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+    case 11: return msm_batch_impl<C, 11>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+    case 12: return msm_batch_impl<C, 12>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+    case 13: return msm_batch_impl<C, 13>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+    default: return KZGX_ERR_INTERNAL;
+  }
+}
+
+bool window_bits_supported(int c) { return c >= 10 && c <= 13; }
+
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st) {
-  if (ctx->c != KZGX_WINDOW_BITS) return KZGX_ERR_INTERNAL;
   return ctx->curve == KZGX_CURVE_BN254
-             ? msm_batch_impl<BN254G1, KZGX_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st)
-             : msm_batch_impl<BLS12381G1, KZGX_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf,
-                                                             st);
+             ? msm_batch_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st)
+             : msm_batch_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
 }
 
 }  // namespace kzgx

@@ -21,7 +21,7 @@ BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 # exported C symbols (must match include/kzg_gpu.h)
 EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
-    "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_sum",
@@ -58,6 +58,8 @@ def lib():
             "kzgx_prof_enable": (ctypes.c_int, [vp, ctypes.c_int]),
             "kzgx_prof_read": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), intp]),
             "kzgx_prof_clear": (ctypes.c_int, [vp]),
+            "kzgx_set_window_bits": (ctypes.c_int, [vp, ctypes.c_int]),
+            "kzgx_set_segment": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_gen_srs_g1": (ctypes.c_int, [vp, u64p, sz, sz]),
             "kzgx_get_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
@@ -129,6 +131,12 @@ class Context:
         cnt = ctypes.c_int(0)
         _chk(lib().kzgx_prof_read(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)), "kzgx_prof_read")
         return ms.value, cnt.value
+
+    def set_window_bits(self, c: int):
+        _chk(lib().kzgx_set_window_bits(self.h, c), "kzgx_set_window_bits")
+
+    def set_segment(self, k: int):
+        _chk(lib().kzgx_set_segment(self.h, k), "kzgx_set_segment")
 
     def prof_clear(self):
         _chk(lib().kzgx_prof_clear(self.h), "kzgx_prof_clear")

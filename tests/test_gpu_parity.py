@@ -167,3 +167,26 @@ def test_vanishing(name, C, n, ctx_factory, oracle_c):
     xs = K.random_scalars(C, n, seed=n)
     got = oracle_c.limbs_to_ints(ctx.vanishing(limbs(xs)))
     assert got == K.linear_roots(C, xs)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("c,seg", [(10, 1), (11, 7), (12, 1000), (13, 64)])
+def test_msm_window_and_segment_variants(name, C, c, seg):
+    """every supported window width / segment length gives the same group element"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        ctx.set_window_bits(c)
+        ctx.set_segment(seg)
+        tau = K.default_tau(C)
+        ctx.gen_srs(tau, 700)
+        n, batch = 700, 3
+        polys = [K.random_scalars(C, n, seed=c * 100 + b) for b in range(batch)]
+        S = np.concatenate([limbs(p) for p in polys])
+        out, inf = ctx.msm_batch(S, n, batch)
+        for b in range(batch):
+            assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b])
+        with pytest.raises(kzgx.KzgxError):
+            ctx.set_window_bits(10)  # table already built
+    finally:
+        ctx.close()
