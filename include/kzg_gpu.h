@@ -114,6 +114,13 @@ int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n
                                    const void* d_z, size_t batch, void* d_out_xy, void* d_out_is_inf, void* d_y,
                                    void* stream);
 
+/* ---- multi-point opening (create_proof(poly, off, len), any len >= 1) ------ */
+/* proof = MSM of q = (P - I) / Z, I the interpolant of P at the len points
+ * xs, Z = prod (X - xs[i]) (trusted_setup.cpp:214-227); all on the GPU.
+ * P is normalized first; deg P < len gives q = 0 -> infinity. */
+int kzgx_prove_range(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t len,
+                     uint64_t* out_xy, int* out_is_inf);
+
 /* ---- scalar-field polynomial ops ----------------------------------------- */
 /* ys[j] = P(xs[j]), j < m */
 int kzgx_poly_eval(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t m, uint64_t* ys);
@@ -124,6 +131,9 @@ int kzgx_poly_interpolate(kzgx_ctx* ctx, const uint64_t* xs, const uint64_t* ys,
 int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z_out);
 
 /* ---- G1 helpers ------------------------------------------------------------ */
+/* *ok = 1 iff xy is a canonical on-curve affine point (ECP_fromOctet's check,
+ * used by deserialize_ECP, src/util.cpp:98-115) */
+int kzgx_g1_validate(kzgx_ctx* ctx, const uint64_t* xy, int* ok);
 /* out = sum of count affine points (is_inf may be NULL); host pointers */
 int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy, int* out_is_inf);
 

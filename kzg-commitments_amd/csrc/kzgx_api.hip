@@ -130,7 +130,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
-                  c.d_poly_ws, ctx->d_srs_canon};
+                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (auto& w : c.ws) {
@@ -324,6 +324,38 @@ int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n
   return kzgx_msm_g1_batch_device(ctx, d_q, nq, batch, nq, d_out_xy, d_out_is_inf, st);
 }
 
+int kzgx_prove_range(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t len,
+                     uint64_t* out_xy, int* out_is_inf) {
+  KZGX_TRY(activate(ctx));
+  if (!xs || !out_xy || !out_is_inf || len == 0 || (n > 0 && !coeffs) || len > (1u << 24)) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  while (n > 0 && (coeffs[4 * (n - 1)] | coeffs[4 * (n - 1) + 1] | coeffs[4 * (n - 1) + 2] | coeffs[4 * (n - 1) + 3]) == 0)
+    n--;  // NTL keeps polynomials normalized
+  if (n > len && n - len > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  hipStream_t st = ctx->c.stream;
+  kzgx::MsmWs* ws = ctx->c.ws_for(st);
+  if (!ws) return KZGX_ERR_ARG;
+  void *d_c = nullptr, *d_x, *d_o;
+  if (n) KZGX_TRY(stage(ctx, 0, n * 32, &d_c));
+  KZGX_TRY(stage(ctx, 1, len * 32, &d_x));
+  KZGX_TRY(stage(ctx, 2, point_words(ctx) * 4 + 16, &d_o));
+  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, n * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xs, len * 32, hipMemcpyHostToDevice, st));
+  size_t nq = 0;
+  if (n > len) {
+    KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ws->q, (n - len) * 32, &ws->q_b));
+    KZGX_TRY(kzgx::prove_range_poly(&ctx->c, (const uint32_t*)d_c, n, (const uint32_t*)d_x, len, ws->q, &nq, st));
+  }
+  uint32_t* d_oi = (uint32_t*)((char*)d_o + point_words(ctx) * 4);
+  KZGX_TRY(kzgx_msm_g1_batch_device(ctx, ws->q, nq, 1, nq, d_o, d_oi, st));
+  uint32_t oi = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, point_words(ctx) * 4, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  *out_is_inf = (int)oi;
+  return KZGX_OK;
+}
+
 int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
                             const uint64_t* zs, size_t batch, uint64_t* out_xy, int* out_is_inf, uint64_t* out_y) {
   KZGX_TRY(activate(ctx));
@@ -402,6 +434,22 @@ int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z
   KZGX_TRY(kzgx::poly_vanishing(&ctx->c, (const uint32_t*)d_x, n, (uint32_t*)d_z, ctx->c.stream));
   KZGX_TRY_HIP(hipMemcpyAsync(z_out, d_z, (n + 1) * 32, hipMemcpyDeviceToHost, ctx->c.stream));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_g1_validate(kzgx_ctx* ctx, const uint64_t* xy, int* ok) {
+  KZGX_TRY(activate(ctx));
+  if (!xy || !ok) return KZGX_ERR_ARG;
+  const size_t pb = point_words(ctx) * 4;
+  void* d_p;
+  KZGX_TRY(stage(ctx, 0, pb + 16, &d_p));
+  uint32_t* d_ok = (uint32_t*)((char*)d_p + pb);
+  KZGX_TRY_HIP(hipMemcpyAsync(d_p, xy, pb, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::g1_validate(&ctx->c, (const uint32_t*)d_p, d_ok, ctx->c.stream));
+  uint32_t v = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(&v, d_ok, 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  *ok = (int)v;
   return KZGX_OK;
 }
 

@@ -75,6 +75,8 @@ struct Ctx {
   std::vector<ProfRec> prof;
   void* d_poly_ws = nullptr;  // scratch for the Fr polynomial kernels
   size_t poly_ws_b = 0;
+  void* d_poly_ws2 = nullptr;  // scratch of the multi-point opening pipeline
+  size_t poly_ws2_b = 0;
   // staging for host-pointer entry points
   void* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_b[4] = {0, 0, 0, 0};
@@ -110,6 +112,7 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
               uint32_t* d_out_inf, hipStream_t st);
 int gen_srs_points(Ctx* ctx, const uint32_t* tau_canon_host, size_t start, size_t n, uint32_t* d_out_canon,
                    hipStream_t st);
+int g1_validate(Ctx* ctx, const uint32_t* d_xy, uint32_t* d_ok, hipStream_t st);
 int g1_sum(Ctx* ctx, const uint32_t* d_xy, const uint32_t* d_inf, size_t count, uint32_t* d_out, uint32_t* d_out_inf,
            hipStream_t st);
 
@@ -119,6 +122,8 @@ int quotient_single(Ctx* ctx, const uint32_t* d_coeffs, size_t n, size_t coeff_s
 int poly_eval(Ctx* ctx, const uint32_t* d_coeffs, size_t n, const uint32_t* d_x, size_t m, uint32_t* d_y,
               hipStream_t st);
 int poly_vanishing(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipStream_t st);
+int prove_range_poly(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_x, size_t len, uint32_t* d_q,
+                     size_t* nq, hipStream_t st);
 int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
                      hipStream_t st);
 

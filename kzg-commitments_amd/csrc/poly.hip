@@ -395,4 +395,71 @@ int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t 
                                         : interpolate_impl<BLS12381Fr>(ctx, d_x, d_y, n, d_coeffs, st);
 }
 
+// --------------------------------------------------------------------------
+// multi-point opening: q = (P - I) / Z  (trusted_setup.cpp:225, NTL sub + div)
+// --------------------------------------------------------------------------
+// out[i] = A[i] - B[i] for i < nout (missing coefficients are zero)
+template <class FR>
+__global__ void k_fr_sub(const uint32_t* __restrict__ A, uint32_t na, const uint32_t* __restrict__ B, uint32_t nb,
+                         uint32_t* __restrict__ out, uint32_t nout) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nout) return;
+  Fe<FR> a = i < na ? fe_load<FR>(A + (size_t)i * FR::N) : fe_zero<FR>();
+  Fe<FR> b = i < nb ? fe_load<FR>(B + (size_t)i * FR::N) : fe_zero<FR>();
+  fe_store<FR>(out + (size_t)i * FR::N, fe_sub<FR>(a, b));
+}
+
+// Quotient of A (na coefficients, overwritten as the remainder) by the monic
+// Z (nz + 1 coefficients): schoolbook long division from the top, one
+// workgroup, the nz coefficient updates of each step spread over its threads.
+template <class FR>
+__global__ __launch_bounds__(1024) void k_div_monic(uint32_t* __restrict__ rem, uint32_t na,
+                                                    const uint32_t* __restrict__ Z, uint32_t nz,
+                                                    uint32_t* __restrict__ q) {
+  constexpr int N = FR::N;
+  const uint32_t nq = na - nz;
+  for (uint32_t k = nq; k-- > 0;) {
+    const Fe<FR> qk = fe_load<FR>(rem + (size_t)(k + nz) * N);
+    if (threadIdx.x == 0) fe_store<FR>(q + (size_t)k * N, qk);
+    const Fe<FR> qm = fe_to_mont<FR>(qk);
+    for (uint32_t j = threadIdx.x; j < nz; j += blockDim.x) {
+      uint32_t* r = rem + (size_t)(k + j) * N;
+      fe_store<FR>(r, fe_sub<FR>(fe_load<FR>(r), fe_mul<FR>(fe_load<FR>(Z + (size_t)j * N), qm)));
+    }
+    __syncthreads();
+  }
+}
+
+template <class FR>
+static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_x, size_t len,
+                                 uint32_t* d_q, size_t* nq_out, hipStream_t st) {
+  constexpr int N = FR::N;
+  const size_t eb = N * 4;
+  *nq_out = 0;
+  if (n <= len) return KZGX_OK;  // deg P < len: I = P, q = 0 (NTL normalizes to the zero polynomial)
+  // workspace: ys (len), I (len), Z (len + 1), A (n)  -- separate from the interpolation scratch
+  void* base;
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (3 * len + 1 + n) * eb, &ctx->poly_ws2_b));
+  base = ctx->d_poly_ws2;
+  uint32_t* ys = (uint32_t*)base;
+  uint32_t* I = ys + len * N;
+  uint32_t* Z = I + len * N;
+  uint32_t* A = Z + (len + 1) * N;
+  KZGX_TRY(poly_eval(ctx, d_P, n, d_x, len, ys, st));
+  KZGX_TRY(poly_interpolate(ctx, d_x, ys, len, I, st));
+  KZGX_TRY(poly_vanishing(ctx, d_x, len, Z, st));
+  hipLaunchKernelGGL(k_fr_sub<FR>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_P, (uint32_t)n, I,
+                     (uint32_t)len, A, (uint32_t)n);
+  hipLaunchKernelGGL(k_div_monic<FR>, dim3(1), dim3(1024), 0, st, A, (uint32_t)n, Z, (uint32_t)len, d_q);
+  KZGX_TRY_HIP(hipGetLastError());
+  *nq_out = n - len;
+  return KZGX_OK;
+}
+
+int prove_range_poly(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_x, size_t len, uint32_t* d_q,
+                     size_t* nq, hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254 ? prove_range_poly_impl<BN254Fr>(ctx, d_P, n, d_x, len, d_q, nq, st)
+                                        : prove_range_poly_impl<BLS12381Fr>(ctx, d_P, n, d_x, len, d_q, nq, st);
+}
+
 }  // namespace kzgx

@@ -81,3 +81,43 @@ int g1_sum(Ctx* ctx, const uint32_t* d_xy, const uint32_t* d_inf, size_t count, 
 }
 
 }  // namespace kzgx
+
+namespace kzgx {
+
+// 1 if the canonical affine point is a valid curve point (coordinates < m,
+// y^2 = x^3 + b), else 0; infinity (all zero) is not a valid octet point
+template <class C>
+__global__ void k_g1_validate(const uint32_t* __restrict__ xy, uint32_t* __restrict__ ok) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  bool lt = true;
+  for (int c = 0; c < 2; c++) {
+    int cmp = 0;  // coordinate vs modulus, most significant word first
+    for (int i = N - 1; i >= 0 && cmp == 0; i--) {
+      const uint32_t a = xy[c * N + i], m = C::Fp::P[i];
+      cmp = a < m ? -1 : (a > m ? 1 : 0);
+    }
+    lt = lt && cmp < 0;
+  }
+  Affine<C> a;
+  const bool finite = affine_from_canonical<C>(xy, a);
+  uint32_t bw[N];
+  for (int i = 0; i < N; i++) bw[i] = i == 0 ? C::BSMALL : 0u;
+  const F29<F> b = f29_to_mont<F>(f29_from_words<F, N>(bw));
+  const F29<F> y2 = f29_sqr<F>(a.y);
+  const F29<F> x3 = f29_mul<F>(f29_sqr<F>(a.x), a.x);
+  const F29<F> d = f29_sub<F>(y2, f29_add<F>(x3, b), F::P4);  // < 6m
+  *ok = (lt && finite && f29_is_zero<F>(d)) ? 1u : 0u;
+}
+
+int g1_validate(Ctx* ctx, const uint32_t* d_xy, uint32_t* d_ok, hipStream_t st) {
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g1_validate<BN254G1>, dim3(1), dim3(64), 0, st, d_xy, d_ok);
+  else
+    hipLaunchKernelGGL(k_g1_validate<BLS12381G1>, dim3(1), dim3(64), 0, st, d_xy, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+}  // namespace kzgx

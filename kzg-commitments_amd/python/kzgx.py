@@ -23,8 +23,8 @@ EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
-    "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_poly_eval",
-    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_sum",
+    "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
+    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
 ]
 
 _lib = None
@@ -69,9 +69,11 @@ def lib():
             "kzgx_quotient_single_batch_device": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, vp, sz, vp, vp]),
             "kzgx_prove_single_batch": (ctypes.c_int, [vp, u64p, sz, sz, u64p, sz, u64p, intp, u64p]),
             "kzgx_prove_single_batch_device": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, vp, vp, vp, vp]),
+            "kzgx_prove_range": (ctypes.c_int, [vp, u64p, sz, u64p, sz, u64p, intp]),
             "kzgx_poly_eval": (ctypes.c_int, [vp, u64p, sz, u64p, sz, u64p]),
             "kzgx_poly_interpolate": (ctypes.c_int, [vp, u64p, u64p, sz, u64p]),
             "kzgx_poly_vanishing": (ctypes.c_int, [vp, u64p, sz, u64p]),
+            "kzgx_g1_validate": (ctypes.c_int, [vp, u64p, intp]),
             "kzgx_g1_sum": (ctypes.c_int, [vp, u64p, intp, sz, u64p, intp]),
         }
         for name, (res, args) in sig.items():
@@ -203,6 +205,16 @@ class Context:
         _chk(lib().kzgx_quotient_single_batch_device(self.h, d_coeffs, n, stride, d_z, batch, d_q, q_stride, d_y,
                                                      stream), "kzgx_quotient_single_batch_device")
 
+    def prove_range(self, coeffs: np.ndarray, xs: np.ndarray):
+        """multi-point opening: MSM of (P - I) / Z for the points xs"""
+        c = as_scalars(coeffs) if len(coeffs) else np.zeros((0, 4), dtype=np.uint64)
+        x = as_scalars(xs)
+        out = np.zeros(2 * self.w64, dtype=np.uint64)
+        inf = ctypes.c_int(0)
+        _chk(lib().kzgx_prove_range(self.h, _p(c) if c.shape[0] else None, c.shape[0], _p(x), x.shape[0], _p(out),
+                                    ctypes.byref(inf)), "kzgx_prove_range")
+        return out, bool(inf.value)
+
     # ---- poly ----
     def poly_eval(self, coeffs: np.ndarray, xs: np.ndarray) -> np.ndarray:
         c = as_scalars(coeffs) if len(coeffs) else np.zeros((0, 4), dtype=np.uint64)
@@ -225,6 +237,12 @@ class Context:
         _chk(lib().kzgx_poly_vanishing(self.h, _p(x) if x.shape[0] else None, x.shape[0], _p(out)),
              "kzgx_poly_vanishing")
         return out
+
+    def g1_validate(self, xy: np.ndarray) -> bool:
+        xy = np.ascontiguousarray(xy, dtype=np.uint64).reshape(2 * self.w64)
+        ok = ctypes.c_int(0)
+        _chk(lib().kzgx_g1_validate(self.h, _p(xy), ctypes.byref(ok)), "kzgx_g1_validate")
+        return bool(ok.value)
 
     def g1_sum(self, pts: np.ndarray, inf=None):
         pts = np.ascontiguousarray(pts, dtype=np.uint64).reshape(-1, 2 * self.w64)

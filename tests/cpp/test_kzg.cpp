@@ -1,0 +1,197 @@
+// C++ API test driver, mirroring /root/reference/testing/testing.cpp through
+// the drop-in kzg:: facade (include/kzg.h) on the GPU.
+//
+// Differences from the reference driver: a fixed tau (the extension ctor) so
+// every commitment / proof is printed and compared bit-for-bit with the
+// golden fixtures by tests/test_gpu_cpp_api.py, and a non-zero exit status
+// on any failed check (the reference never fails its build).
+// verify_proof is not exercised: the pairing path is a later row.
+//
+// usage: test_kzg <curve 0|1> <tau hex> <blob dir>
+#include <kzg.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+static int failures = 0;
+
+static void check_test(bool status, const std::string& name) {
+  std::cout << (status ? "PASSED" : "FAILED") << " [" << name << "]" << std::endl;
+  if (!status) failures++;
+}
+
+static std::string hex(const std::vector<uint8_t>& b) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (uint8_t x : b) {
+    s += d[x >> 4];
+    s += d[x & 15];
+  }
+  return s;
+}
+
+static kzg::Fr fr_from_hex(const std::string& h) {
+  std::string s = h.rfind("0x", 0) == 0 ? h.substr(2) : h;
+  std::vector<uint8_t> le;
+  for (int i = (int)s.size(); i > 0; i -= 2) {
+    std::string byte = s.substr(i >= 2 ? i - 2 : 0, i >= 2 ? 2 : 1);
+    le.push_back((uint8_t)strtol(byte.c_str(), nullptr, 16));
+  }
+  return kzg::Fr::from_le_bytes(le.data(), le.size());
+}
+
+// testing.cpp:406-413
+static std::vector<uint8_t> from_hex(const std::string& s) {
+  std::vector<uint8_t> res;
+  for (size_t i = 0; i < s.size(); i += 2) res.push_back((uint8_t)strtol(s.substr(i, 2).c_str(), nullptr, 16));
+  return res;
+}
+
+static void emit_commit(const std::string& name, kzg::commit c) {
+  std::cout << "COMMIT\t" << name << "\t" << hex(c.serialize()) << std::endl;
+}
+
+static void emit_proof(const std::string& name, int off, int len, kzg::proof p) {
+  std::cout << "PROOF\t" << name << "\t" << off << "\t" << len << "\t" << hex(p.serialize()) << std::endl;
+}
+
+template <class F>
+static bool throws(F f) {
+  try {
+    f();
+  } catch (const std::invalid_argument&) {
+    return true;
+  }
+  return false;
+}
+
+static void string_case(const kzg::Fr& tau, const std::string& name, const std::string& data, int setup,
+                        std::vector<std::pair<int, int>> proofs) {
+  kzg::trusted_setup kzg(setup, tau);
+  kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string(data));
+  // serialize round trip (general_test, testing.cpp:319-327)
+  kzg::poly again = kzg::poly::deserialize(poly.serialize());
+  check_test(again.get_poly() == poly.get_poly(), name + ", poly serialize round trip");
+  std::cout << "POLY\t" << name << "\t" << hex(poly.serialize()) << std::endl;
+  if (poly.degree() + 1 >= setup) {
+    check_test(throws([&] { kzg.create_commit(poly); }), name + ", commit is invalid");
+    return;
+  }
+  kzg::commit c = kzg.create_commit(poly);
+  check_test(kzg.verify_commit(c, poly), name + ", commit verification");
+  kzg::commit c2 = kzg::commit::deserialize(c.serialize());
+  check_test(kzg.verify_commit(c2, poly), name + ", commit serialize round trip");
+  emit_commit(name, c);
+  for (auto& pr : proofs) emit_proof(name, pr.first, pr.second, kzg.create_proof(poly, pr.first, pr.second));
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    std::cerr << "usage: test_kzg <curve> <tau hex> <blob dir>" << std::endl;
+    return 2;
+  }
+  kzg::init(atoi(argv[1]));
+  const kzg::Fr tau = fr_from_hex(argv[2]);
+  const std::string dir = argv[3];
+
+  // invalid_setup_test (testing.cpp:153-163)
+  check_test(throws([&] { kzg::trusted_setup k(0, tau); }), "empty polynomial is invalid");
+  check_test(throws([&] { kzg::trusted_setup k(1, tau); }), "0 degree polynomial is invalid");
+  check_test(throws([&] { kzg::trusted_setup k(0); }), "random setup: 0 is invalid");
+
+  // empty_proof_test (testing.cpp:129-137)
+  {
+    kzg::trusted_setup kzg(128, tau);
+    kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string("some data here"));
+    check_test(throws([&] { kzg.create_proof(poly, 5, 0); }), "empty proof is invalid");
+  }
+
+  string_case(tau, "poly_degree_1_test K", "K", 2, {{0, 1}});
+  string_case(tau, "poly_degree_1_test AB", "AB", 2, {});
+  string_case(tau, "poly_degree_10_test 11 chars", "CEBIDKAGFJH", 11, {});
+  string_case(tau, "poly_degree_10_test", "CEBIDAGFJH", 11, {{2, 3}});
+  string_case(tau, "high_poly_degree_test 150",
+              "fa37JncCHryDsbzayy4cBWDxS22JjzhMaiRrV41mtzxlYvKWrO72tK0LK0e1zLOZ2nOXpPIhMFSv8kP07U20o0J90xA0GWXIIwo7J4o"
+              "gHFZQxwQ2RQ0DRJKRETPVzxlFrXL8b7mtKLHIGhIh5JuWcF",
+              150, {});
+  string_case(tau, "high_poly_degree_test 149",
+              "wrgJKdE3t5bECALy3eKIwYxEF3V7Z8KTx0nFe1IX5tjH22F5gXOa5LnIMIQuOiNJj8YL8rqDiZSkZfoEDAmGTXXqqvkCd5WKE2fMtVXa2zKa"
+              "e6opGY4i6bYuUG67LaSXd5tUbO4bNPB0TxnkWrSaQ",
+              150, {{49, 57}});
+  string_case(tau, "empty_verify_test", "some data here", 128, {{7, 2}});
+  string_case(tau, "README example", "hello there my name is bob", 128, {{0, 5}, {15, 7}, {23, 3}});
+  string_case(tau, "signed chars", std::string("\x80\xff\x7f\x00\x41", 5), 16, {{1, 2}});
+
+  // chunking_test / chunking_invalid_args_test (testing.cpp:254-311)
+  {
+    kzg::trusted_setup kzg(128, tau);
+    unsigned char data[] = "ysudYUGdghv675d";
+    check_test(throws([&] { kzg::blob::from_bytes(data, 0, sizeof(data), 3); }), "chunking, chunks do not divide data");
+    const int chunks[3] = {1, 2, 4};
+    const int boff[3] = {3, 2, 4}, blen[3] = {9, 10, 8};
+    for (int t = 0; t < 3; t++) {
+      const int cs = chunks[t];
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_bytes(data, 0, sizeof(data), cs));
+      kzg::commit c = kzg.create_commit(poly);
+      std::string name = "chunking_test chunk " + std::to_string(cs);
+      check_test(kzg.verify_commit(c, poly), name + ", commit verification");
+      emit_commit(name, c);
+      emit_proof(name, boff[t] / cs, blen[t] / cs, kzg.create_proof(poly, boff[t], blen[t], cs));
+    }
+    kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_bytes(data, 0, sizeof(data), 1));
+    check_test(throws([&] { kzg.create_proof(poly, 0, 5, 4); }), "chunking invalid args, invalid byte length");
+    check_test(throws([&] { kzg.create_proof(poly, 2, 8, 4); }), "chunking invalid args, invalid byte offset");
+    check_test(throws([&] { kzg.create_proof(poly, 0, 32, 32); }), "chunk size above MAX_CHUNK_BYTES");
+  }
+
+  // eth_blob_test (testing.cpp:53-102), commits and chunk proofs
+  {
+    kzg::trusted_setup kzg(5000, tau);
+    const char* files[2] = {"blob2.txt", "blob1.txt"};
+    const int offs[2][3] = {{0, 10, 62}, {7, 100, 4224}};
+    const int lens[2][3] = {{1, 4, 4}, {1, 4, 4}};
+    for (int f = 0; f < 2; f++) {
+      std::ifstream in(dir + "/" + files[f]);
+      std::stringstream buf;
+      buf << in.rdbuf();
+      std::vector<uint8_t> bytes = from_hex(buf.str());
+      int zero_pad = MAX_CHUNK_BYTES - (bytes.size() % MAX_CHUNK_BYTES);
+      for (int i = 0; i < zero_pad; i++) bytes.push_back(0);
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_bytes(bytes.data(), 0, bytes.size(), MAX_CHUNK_BYTES));
+      kzg::commit c = kzg.create_commit(poly);
+      std::string name = std::string("eth_blob_test ") + (f ? "blob1" : "blob2");
+      check_test(kzg.verify_commit(c, poly), name + ", commit verification");
+      emit_commit(name, c);
+      for (int k = 0; k < 3; k++) emit_proof(name, offs[f][k], lens[f][k], kzg.create_proof(poly, offs[f][k], lens[f][k]));
+    }
+  }
+
+  // batched extensions agree with the one-at-a-time API
+  {
+    kzg::trusted_setup kzg(300, tau);
+    std::vector<kzg::poly> ps;
+    for (int i = 0; i < 5; i++) ps.push_back(kzg::poly::from_blob(kzg::blob::from_string(std::string(37 * (i + 1), 'a' + i))));
+    auto cs = kzg.create_commits(ps);
+    bool same = true;
+    for (int i = 0; i < 5; i++) same &= cs[i].get_curve_point() == kzg.create_commit(ps[i]).get_curve_point();
+    check_test(same, "create_commits == create_commit");
+    auto prs = kzg.create_proofs(ps[4], {0, 3, 184});
+    same = prs[1].get_curve_point() == kzg.create_proof(ps[4], 3, 1).get_curve_point();
+    check_test(same, "create_proofs == create_proof");
+  }
+
+  // bad octets deserialize to infinity (util.cpp:107-112)
+  {
+    std::vector<uint8_t> junk(4 + 1 + 2 * (kzg::curve() == KZGX_CURVE_BN254 ? 32 : 48), 0x11);
+    uint32_t len = (uint32_t)junk.size() - 4;
+    std::memcpy(junk.data(), &len, 4);
+    junk[4] = 4;
+    check_test(kzg::commit::deserialize(junk).get_curve_point().inf, "off-curve octet decodes to infinity");
+  }
+
+  std::cout << "FAILURES\t" << failures << std::endl;
+  return failures ? 1 : 0;
+}
