@@ -104,7 +104,8 @@ KZGX_DEV void load_scalar(const uint32_t* p, uint32_t (&s)[8]) {
 // pass 1: per-MSM bucket histogram
 template <int CB>
 __global__ __launch_bounds__(256) void k_msm_count(const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words,
-                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ counts) {
+                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ counts,
+                                                   uint32_t point_base, uint32_t point_stride) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   __shared__ uint32_t hist[NB];
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(256) void k_msm_count(const uint32_t* __restrict__ 
   for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && !inf[i]) {
+  if (i < n && !inf[point_base + b * point_stride + i]) {
     uint32_t s[8];
     load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
     uint32_t carry = 0;
@@ -163,7 +164,8 @@ template <int CB>
 __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
                                                      size_t stride_words, const uint8_t* __restrict__ inf,
                                                      uint32_t* __restrict__ cursors, uint32_t* __restrict__ entries,
-                                                     size_t emax, uint32_t n_srs) {
+                                                     size_t emax, uint32_t n_srs, uint32_t point_base,
+                                                     uint32_t point_stride) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   __shared__ uint32_t lcount[NB];
@@ -174,7 +176,8 @@ __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict_
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   int dig[W];
   uint32_t rank[W];
-  const bool live = i < n && !inf[i];
+  const uint32_t ig = point_base + b * point_stride + i;  // SRS index of this scalar
+  const bool live = i < n && !inf[ig];
   if (live) {
     uint32_t s[8];
     load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict_
       int d = dig[w];
       if (d != 0) {
         uint32_t k = (uint32_t)((d < 0 ? -d : d) - 1);
-        out[lbase[k] + rank[w]] = ((uint32_t)w * n_srs + i) | (d < 0 ? 0x80000000u : 0u);
+        out[lbase[k] + rank[w]] = ((uint32_t)w * n_srs + ig) | (d < 0 ? 0x80000000u : 0u);
       }
     }
   }
@@ -321,10 +324,12 @@ KZGX_DEV Xyzz<C> xyzz_shfl(const Xyzz<C>& p, int src) {
 //   R'_g = sum_i R_{4g+i} + s (T_{4g+1} + 2 T_{4g+2} + 3 T_{4g+3}),
 //   T'_g = sum_i T_{4g+i},   scale' = 4 s,
 // which preserves  sum_t R_t + s sum_t t T_t.  When one pair is left, R is
-// the MSM value; lane 0 converts it to canonical affine.
+// the MSM value; lane 0 converts it to canonical affine, or stores the XYZZ
+// point to xyzz_out (chunked single MSMs, summed by k_xyzz_sum).
 template <class C>
 __global__ __launch_bounds__(256) void k_msm_window_tail(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
-                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                         uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -381,10 +386,41 @@ __global__ __launch_bounds__(256) void k_msm_window_tail(const uint32_t* __restr
     s *= gsz;
   }
   if (lane == 0) {
+    if (xyzz_out) {
+      xyzz_store<C>(xyzz_out + (size_t)b * XW, R);
+      return;
+    }
     Affine<C> a;
     bool fin = xyzz_to_affine<C>(R, a);
     affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
     out_inf[b] = fin ? 0u : 1u;
+  }
+}
+
+// sum of count XYZZ points -> canonical affine (one 256-thread workgroup:
+// strided per-thread sums, then an LDS tree)
+template <class C>
+__global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ pts, uint32_t count,
+                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  extern __shared__ uint32_t lds[];
+  const uint32_t t = threadIdx.x;
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t i = t; i < count; i += blockDim.x) acc = xyzz_add<C>(acc, xyzz_load<C>(pts + (size_t)i * XW));
+  xyzz_store<C>(lds + t * XW, acc);
+  __syncthreads();
+  for (uint32_t h = blockDim.x / 2; h >= 1; h >>= 1) {
+    if (t < h) {
+      acc = xyzz_add<C>(acc, xyzz_load<C>(lds + (t + h) * XW));
+      xyzz_store<C>(lds + t * XW, acc);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    Affine<C> a;
+    bool fin = xyzz_to_affine<C>(acc, a);
+    affine_to_canonical<C>(out, a, fin);
+    *out_inf = fin ? 0u : 1u;
   }
 }
 
@@ -407,7 +443,8 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
 
 template <class C, int CB>
 int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
-                   uint32_t* d_out_inf, hipStream_t st) {
+                   uint32_t* d_out_inf, hipStream_t st, uint32_t point_base, uint32_t point_stride,
+                   uint32_t* xyzz_out) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   const uint32_t K = ctx->seg_k;
@@ -430,7 +467,8 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   dim3 gs((unsigned)((n + 255) / 256), (unsigned)batch);
   {
     ProfScope p(ctx, st, "msm_count");
-    hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts);
+    hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts,
+                       point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_scan");
@@ -439,7 +477,7 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   {
     ProfScope p(ctx, st, "msm_scatter");
     hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
-                       ws.cursors, ws.entries, emax, (uint32_t)ctx->n_srs);
+                       ws.cursors, ws.entries, emax, (uint32_t)ctx->n_srs, point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_accum");
@@ -453,7 +491,7 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB, K,
                        smax, ws.bsum, ws.heads, ws.tails, ws.rt);
     hipLaunchKernelGGL(k_msm_window_tail<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
-                       (uint32_t)batch, d_out, d_out_inf);
+                       (uint32_t)batch, d_out, d_out_inf, xyzz_out);
   }
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
@@ -466,23 +504,60 @@ int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
 
 template <class C>
 static int msm_batch_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
-                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t point_base,
+                       uint32_t point_stride, uint32_t* xyzz_out) {
   switch (ctx->c) {
-    case 10: return msm_batch_impl<C, 10>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
-    case 11: return msm_batch_impl<C, 11>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
-    case 12: return msm_batch_impl<C, 12>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
-    case 13: return msm_batch_impl<C, 13>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+    case 10: return msm_batch_impl<C, 10>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
+    case 11: return msm_batch_impl<C, 11>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
+    case 12: return msm_batch_impl<C, 12>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
+    case 13: return msm_batch_impl<C, 13>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
     default: return KZGX_ERR_INTERNAL;
   }
 }
 
 bool window_bits_supported(int c) { return c >= 10 && c <= 13; }
 
+// One large MSM is cut into chunks of MSM_CHUNK points that run as a batch
+// of independent MSMs over consecutive SRS ranges (point_stride), each
+// reduced to an XYZZ partial, then summed by one workgroup.  Every chunk has
+// the bucket occupancy the batched path is tuned for, so a degree-2^20
+// commitment fills the chip instead of waiting on 2^(c-1) very long buckets.
+constexpr size_t MSM_CHUNK = 4096;
+
+template <class C>
+static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                              hipStream_t st) {
+  const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+  const size_t full = n / MSM_CHUNK, rest = n % MSM_CHUNK;
+  const size_t parts = full + (rest ? 1 : 0);
+  MsmWs* ws = ctx->ws_for(st);
+  if (!ws) return KZGX_ERR_ARG;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws->parts, parts * XB, &ws->parts_b));
+  uint32_t* parts_buf = ws->parts;
+  if (full)
+    KZGX_TRY(msm_batch_c<C>(ctx, d_scalars, MSM_CHUNK, full, MSM_CHUNK * 8, d_out, d_out_inf, st, 0, MSM_CHUNK,
+                            parts_buf));
+  if (rest) {
+    // the tail chunk: a batch of one over SRS points [full * CHUNK, n)
+    KZGX_TRY(msm_batch_c<C>(ctx, d_scalars + full * MSM_CHUNK * 8, rest, 1, rest * 8, d_out, d_out_inf, st,
+                            (uint32_t)(full * MSM_CHUNK), 0, parts_buf + full * xyzz_words<C>()));
+  }
+  {
+    ProfScope p(ctx, st, "msm_reduce");
+    hipLaunchKernelGGL(k_xyzz_sum<C>, dim3(1), dim3(256), 256 * XB, st, parts_buf, (uint32_t)parts, d_out, d_out_inf);
+  }
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st) {
-  return ctx->curve == KZGX_CURVE_BN254
-             ? msm_batch_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st)
-             : msm_batch_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
+  const bool bn = ctx->curve == KZGX_CURVE_BN254;
+  if (batch == 1 && n >= 4 * MSM_CHUNK)
+    return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
+              : msm_single_chunked<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
+  return bn ? msm_batch_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr)
+            : msm_batch_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr);
 }
 
 }  // namespace kzgx

@@ -1,0 +1,74 @@
+"""Multi-GPU sharding of one large commitment (BASELINE.json configs[4]).
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm).
+The points of Σ c_i [tau^i]G1 are split into contiguous ranges; every rank
+generates its own SRS slice [tau^(start+i)]G1 on its GPU and computes the
+partial MSM of its range.  EC addition is not an RCCL reduction operator, so
+the one exchange step is an all-gather of the N partial affine points
+(N x (2 W64 + 1) int64 words: a few hundred bytes over xGMI) followed by an
+exact fold on every rank.  The fold is order-independent after affine
+normalization, so every rank holds the bit-exact commitment.
+
+The partial-MSM and fold callables are injected so the same driver runs
+with the GPU (kzgx.Context) in bench.py and with the CPU oracle in the
+gloo tests (tests/test_dist_gloo.py).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+
+
+def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous [start, start + count) of n items for rank; remainders go to the first ranks."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def pack_point(xy: np.ndarray, inf: bool, w64: int) -> np.ndarray:
+    out = np.zeros(2 * w64 + 1, dtype=np.int64)
+    out[: 2 * w64] = np.asarray(xy, dtype=np.uint64).view(np.int64)[: 2 * w64]
+    out[-1] = 1 if inf else 0
+    return out
+
+
+def unpack_points(buf: np.ndarray, w64: int):
+    buf = np.asarray(buf, dtype=np.int64).reshape(-1, 2 * w64 + 1)
+    return buf[:, : 2 * w64].view(np.uint64), buf[:, -1].astype(bool)
+
+
+def sharded_commit(n: int, world: int, rank: int, w64: int,
+                   partial_msm: Callable[[int, int], Tuple[np.ndarray, bool]],
+                   all_gather: Callable[[np.ndarray], np.ndarray],
+                   fold: Callable[[np.ndarray, np.ndarray], Tuple[np.ndarray, bool]],
+                   ) -> Tuple[np.ndarray, bool]:
+    """partial_msm(start, count) -> (xy, inf) of this rank's slice;
+    all_gather(packed) -> (world, 2 W64 + 1) array of every rank's packed point;
+    fold(points, infs) -> (xy, inf) sum of the gathered points."""
+    start, count = shard_range(n, world, rank)
+    if count:
+        xy, inf = partial_msm(start, count)
+    else:
+        xy, inf = np.zeros(2 * w64, dtype=np.uint64), True
+    gathered = all_gather(pack_point(xy, inf, w64))
+    pts, infs = unpack_points(gathered, w64)
+    return fold(pts, infs)
+
+
+def torch_all_gather(dist, device: Optional[object] = None):
+    """all_gather callable over torch.distributed (RCCL on GPU, gloo on CPU)."""
+    import torch
+
+    def gather(packed: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(np.ascontiguousarray(packed))
+        if device is not None:
+            t = t.to(device)
+        outs = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(outs, t)
+        return torch.stack(outs).cpu().numpy()
+
+    return gather

@@ -190,3 +190,16 @@ def test_msm_window_and_segment_variants(name, C, c, seg):
             ctx.set_window_bits(10)  # table already built
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [16384, 16385, 20000, 70001])
+def test_large_single_msm_chunked(name, C, n, ctx_factory):
+    """single MSMs of >= 4 chunks run as a chunked batch + XYZZ tree sum"""
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    ctx.gen_srs(tau, n + 3)
+    sc = K.random_scalars(C, n, seed=n)
+    sc[n // 2] = 0
+    out, inf = ctx.msm(limbs(sc))
+    assert pt(name, out, inf) == K.commit_via_tau(C, tau, sc)
