@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
+    ap.add_argument("--split", type=int, default=1, help="sub-batches (each on its own stream) per batch")
     ap.add_argument("--cpu-sample", type=int, default=3, help="commits (+ as many proofs) timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -130,19 +131,26 @@ def main():
     d_pout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
     d_pinf = torch.zeros((B,), dtype=torch.int32, device=dev)
     d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
-    # commits and proofs of a step are independent: two streams so the
-    # latency-bound tail of one batch overlaps the accumulation of the other
-    stream = torch.cuda.Stream(device=dev)
-    stream2 = torch.cuda.Stream(device=dev)
-    sp = stream.cuda_stream
-    sp2 = stream2.cuda_stream
+    # the commits and proofs of a step are independent: each batch is cut into
+    # `split` sub-batches on their own streams so the latency-bound phases
+    # (bucket sums, tails) of one overlap the accumulation of another
+    S = max(1, args.split)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2 * S)]
+    stream = streams[0]
     cstride = 0 if args.workload == "cfg3" else n
+    cut = [B * s // S for s in range(S + 1)]
 
     def step():
-        if args.workload != "cfg3":
-            ctx.msm_batch_device(d_coeffs.data_ptr(), n, B, n, d_cout.data_ptr(), d_cinf.data_ptr(), sp)
-        ctx.prove_single_batch_device(d_coeffs.data_ptr(), n, cstride, d_z.data_ptr(), B, d_pout.data_ptr(),
-                                      d_pinf.data_ptr(), d_y.data_ptr(), sp2)
+        for s in range(S):
+            lo, hi = cut[s], cut[s + 1]
+            if hi == lo:
+                continue
+            if args.workload != "cfg3":
+                ctx.msm_batch_device(d_coeffs[lo].data_ptr(), n, hi - lo, n, d_cout[lo].data_ptr(),
+                                     d_cinf[lo:].data_ptr(), streams[2 * s].cuda_stream)
+            ctx.prove_single_batch_device(d_coeffs[0 if cstride == 0 else lo].data_ptr(), n, cstride,
+                                          d_z[lo].data_ptr(), hi - lo, d_pout[lo].data_ptr(), d_pinf[lo:].data_ptr(),
+                                          d_y[lo].data_ptr(), streams[2 * s + 1].cuda_stream)
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
 
@@ -160,12 +168,14 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     ev0.record(stream)
-    stream2.wait_event(ev0)
+    for s in streams[1:]:
+        s.wait_event(ev0)
     for _ in range(args.steps):
         step()
-    ev_b = torch.cuda.Event()
-    ev_b.record(stream2)
-    stream.wait_event(ev_b)
+    for s in streams[1:]:
+        ev_b = torch.cuda.Event()
+        ev_b.record(s)
+        stream.wait_event(ev_b)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
@@ -294,6 +304,7 @@ def main():
                 "parallelism": "dp%d (independent batches, no collective)" % world,
                 "window_bits": args.window_bits,
                 "segment": args.segment,
+                "streams": 2 * max(1, args.split),
             },
             "roofline": {
                 "kernel": "msm_accum",

@@ -93,7 +93,8 @@ KZGX_DEV Xyzz<C> xyzz_dbl_affine_impl(const Affine<C>& a) {
   F29<F> xx = f29_sqr<F>(a.x);
   F29<F> M = f29_add<F>(f29_add<F>(xx, xx), xx);        // < 6m
   F29<F> X3 = f29_sub<F>(f29_sqr<F>(M), f29_add<F>(S, S), F::P4);  // < 6m
-  F29<F> Y3 = f29_sub<F>(f29_mul<F>(M, f29_sub<F>(S, X3, F::P8)), f29_mul<F>(W, a.y), F::P2);  // < 4m
+  // M (S - X3) - W y as one reduction: + W (4m - y) = - W y mod m; < 60m^2 + 8m^2
+  F29<F> Y3 = f29_mul2<F>(M, f29_sub<F>(S, X3, F::P8), W, f29_sub<F>(f29_zero<F>(), a.y, F::P4));  // < 2m
   r.X = X3;
   r.Y = Y3;
   r.ZZ = V;
@@ -114,7 +115,7 @@ KZGX_DEV Xyzz<C> xyzz_dbl_impl(const Xyzz<C>& p) {
   F29<F> xx = f29_sqr<F>(p.X);
   F29<F> M = f29_add<F>(f29_add<F>(xx, xx), xx);        // < 6m
   F29<F> X3 = f29_sub<F>(f29_sqr<F>(M), f29_add<F>(S, S), F::P4);  // < 6m
-  F29<F> Y3 = f29_sub<F>(f29_mul<F>(M, f29_sub<F>(S, X3, F::P8)), f29_mul<F>(W, p.Y), F::P2);
+  F29<F> Y3 = f29_mul2<F>(M, f29_sub<F>(S, X3, F::P8), W, f29_sub<F>(f29_zero<F>(), p.Y, F::P4));  // < 2m
   r.X = X3;
   r.Y = Y3;
   r.ZZ = f29_mul<F>(V, p.ZZ);
@@ -140,7 +141,8 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
   F29<F> Q = f29_mul<F>(p.X, PP);
   Xyzz<C> r;
   r.X = f29_sub<F>(f29_sqr<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);       // < 8m
-  r.Y = f29_sub<F>(f29_mul<F>(R, f29_sub<F>(Q, r.X, F::P8)), f29_mul<F>(p.Y, PPP), F::P2);  // < 4m
+  // R (Q - X3) - Y1 PPP with one reduction: < 60m^2 + 8m^2 -> < 2m
+  r.Y = f29_mul2<F>(R, f29_sub<F>(Q, r.X, F::P8), f29_sub<F>(f29_zero<F>(), p.Y, F::P4), PPP);
   r.ZZ = f29_mul<F>(p.ZZ, PP);
   r.ZZZ = f29_mul<F>(p.ZZZ, PPP);
   return r;
@@ -160,14 +162,14 @@ KZGX_DEV Xyzz<C> xyzz_add_impl(const Xyzz<C>& p, const Xyzz<C>& q) {
   F29<F> R = f29_sub<F>(S2, S1, F::P2);                 // < 4m
   F29<F> PP = f29_sqr<F>(P);
   if (f29_is_zero_lt2m<F>(PP)) {
-    if (f29_is_zero<F>(R)) return xyzz_dbl<C>(p);
+    if (f29_is_zero<F>(R)) return xyzz_dbl_impl<C>(p);  // inline: no call frame in callers' loops
     return xyzz_inf<C>();
   }
   F29<F> PPP = f29_mul<F>(P, PP);
   F29<F> Q = f29_mul<F>(U1, PP);
   Xyzz<C> r;
   r.X = f29_sub<F>(f29_sqr<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);
-  r.Y = f29_sub<F>(f29_mul<F>(R, f29_sub<F>(Q, r.X, F::P8)), f29_mul<F>(S1, PPP), F::P2);
+  r.Y = f29_mul2<F>(R, f29_sub<F>(Q, r.X, F::P8), f29_sub<F>(f29_zero<F>(), S1, F::P2), PPP);  // < 2m
   r.ZZ = f29_mul<F>(f29_mul<F>(p.ZZ, q.ZZ), PP);
   r.ZZZ = f29_mul<F>(f29_mul<F>(p.ZZZ, q.ZZZ), PPP);
   return r;

@@ -125,6 +125,42 @@ KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
   return t;
 }
 
+// (a b + c d) / R mod m with ONE reduction (sum of products before REDC).
+// Column sums stay below 2^64: 2L products + L reduction terms < 2^58 each.
+// Output < 2m when a b + c d < (R / m) m^2.
+template <class F>
+KZGX_DEV F29<F> f29_mul2(const F29<F>& a, const F29<F>& b, const F29<F>& c, const F29<F>& d) {
+  constexpr int L = F::L;
+  uint32_t q[L];
+  F29<F> t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) {
+        acc += (uint64_t)a.v[i] * b.v[j];
+        acc += (uint64_t)c.v[i] * d.v[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+    }
+    if (k < L) {
+      q[k] = ((uint32_t)acc * F::INV) & M29;
+      acc += (uint64_t)q[k] * F::P[0];
+    } else {
+      t.v[k - L] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+  }
+  t.v[L - 1] = (uint32_t)acc;
+  return t;
+}
+
 // Montgomery square: cross products once, against a doubled operand
 template <class F>
 KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {

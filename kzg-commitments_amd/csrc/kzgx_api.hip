@@ -134,7 +134,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (auto& w : c.ws) {
-    void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum, w.heads, w.tails, w.rt, w.q, w.parts};
+    void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum, w.heads, w.tails, w.tailk, w.rt, w.q, w.parts};
     for (void* p : wb)
       if (p) (void)hipFree(p);
   }

@@ -8,6 +8,14 @@
 
 #include "../../include/kzg_gpu.h"
 
+#ifndef KZGX_ACCUM_WAVES
+#define KZGX_ACCUM_WAVES 3  // min waves per SIMD for k_msm_accum (VGPR budget)
+#endif
+
+#ifndef KZGX_BS_WAVES
+#define KZGX_BS_WAVES 2  // min waves per SIMD for k_msm_bucket_sums
+#endif
+
 #ifndef KZGX_WINDOW_BITS
 #define KZGX_WINDOW_BITS 12  // default signed-digit window (10..13 supported)
 #endif
@@ -30,9 +38,10 @@ int hip_fail(hipError_t e);
 
 struct MsmWs {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursors = nullptr, *entries = nullptr;
-  uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr, *rt = nullptr, *q = nullptr, *parts = nullptr;
-  size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0, rt_b = 0,
-         q_b = 0, parts_b = 0;
+  uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr, *tailk = nullptr, *rt = nullptr, *q = nullptr,
+           *parts = nullptr;
+  size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0, tailk_b = 0,
+         rt_b = 0, q_b = 0, parts_b = 0;
   hipStream_t owner = nullptr;  // workspaces are per stream so calls on
   bool used = false;            // different streams may run concurrently
 };

@@ -209,12 +209,14 @@ __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict_
 }
 
 // pass 4: balanced bucket accumulation, K entries per thread
+constexpr uint32_t NO_TAIL = 0xffffffffu;
+
 template <class C>
-__global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ entries, size_t emax,
+__global__ __launch_bounds__(256, KZGX_ACCUM_WAVES) void k_msm_accum(const uint32_t* __restrict__ entries, size_t emax,
                                                    const uint32_t* __restrict__ offsets, uint32_t nb,
                                                    const uint32_t* __restrict__ table, uint32_t K, size_t smax,
                                                    uint32_t* __restrict__ bsum, uint32_t* __restrict__ heads,
-                                                   uint32_t* __restrict__ tails) {
+                                                   uint32_t* __restrict__ tails, uint32_t* __restrict__ tailk) {
   constexpr int PW = affine_words<C>();
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
@@ -256,13 +258,39 @@ __global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ 
     acc = xyzz_add_affine_impl<C>(acc, a);
   }
   uint32_t* dst;
-  if (before)
+  uint32_t tk = NO_TAIL;
+  if (before) {
     dst = heads + ((size_t)b * smax + seg) * XW;
-  else if (next > end)
+  } else if (next > end) {
     dst = tails + ((size_t)b * smax + seg) * XW;
-  else
+    tk = k;
+  } else {
     dst = bsum + ((size_t)b * nb + k) * XW;
+  }
   xyzz_store<C>(dst, acc);
+  tailk[(size_t)b * smax + seg] = tk;
+}
+
+// pass 4b: buckets that straddle segments.  The segment holding the start
+// of such a bucket stored its partial as a tail (tailk = bucket); the later
+// segments of the bucket stored heads.  One thread per segment with a tail
+// sums tail + heads into bsum, so the bucket pass below is branch-free.
+template <class C>
+__global__ __launch_bounds__(256) void k_msm_fixup(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
+                                                   size_t smax, const uint32_t* __restrict__ heads,
+                                                   const uint32_t* __restrict__ tails,
+                                                   const uint32_t* __restrict__ tailk, uint32_t* __restrict__ bsum) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t b = blockIdx.y;
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t* off = offsets + (size_t)b * (nb + 1);
+  if ((size_t)seg * K >= off[nb]) return;
+  const uint32_t k = tailk[(size_t)b * smax + seg];
+  if (k == NO_TAIL) return;
+  const uint32_t e1 = off[k + 1];
+  Xyzz<C> acc = xyzz_load<C>(tails + ((size_t)b * smax + seg) * XW);
+  for (uint32_t s = seg + 1; (size_t)s * K < e1; s++) acc = xyzz_add<C>(acc, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
+  xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
 }
 
 // pass 5a: finish the buckets and their first-level weighted sums.
@@ -272,31 +300,20 @@ __global__ __launch_bounds__(256) void k_msm_accum(const uint32_t* __restrict__ 
 constexpr uint32_t RED_J = 8;
 
 template <class C>
-__global__ __launch_bounds__(256) void k_msm_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
-                                                         size_t smax, const uint32_t* __restrict__ bsum,
-                                                         const uint32_t* __restrict__ heads,
-                                                         const uint32_t* __restrict__ tails,
-                                                         uint32_t* __restrict__ rt) {
+__global__ __launch_bounds__(256, KZGX_BS_WAVES) void k_msm_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb,
+                                                                        const uint32_t* __restrict__ bsum,
+                                                                        uint32_t* __restrict__ rt) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
   const uint32_t T1 = nb / RED_J;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T1) return;
-  const uint32_t* off = offsets + (size_t)b * (nb + 1);
+  const uint32_t* off = offsets + (size_t)b * (nb + 1) + t * RED_J;
+  const uint32_t* src = bsum + ((size_t)b * nb + t * RED_J) * XW;
   Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
   for (int j = (int)RED_J - 1; j >= 0; j--) {
-    const uint32_t k = t * RED_J + (uint32_t)j;
-    const uint32_t o0 = off[k], o1 = off[k + 1];
     Xyzz<C> bk = xyzz_inf<C>();
-    if (o1 > o0) {
-      const uint32_t s0 = o0 / K, s1 = (o1 - 1) / K;
-      if (s0 == s1) {
-        bk = xyzz_load<C>(bsum + ((size_t)b * nb + k) * XW);
-      } else {
-        bk = xyzz_load<C>(tails + ((size_t)b * smax + s0) * XW);
-        for (uint32_t s = s0 + 1; s <= s1; s++) bk = xyzz_add_impl<C>(bk, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
-      }
-    }
+    if (off[j + 1] > off[j]) bk = xyzz_load<C>(src + (size_t)j * XW);  // empty buckets were never written
     run = xyzz_add_impl<C>(run, bk);
     sum = xyzz_add_impl<C>(sum, run);
   }
@@ -305,95 +322,59 @@ __global__ __launch_bounds__(256) void k_msm_bucket_sums(const uint32_t* __restr
   xyzz_store<C>(dst + XW, run);
 }
 
+// pass 5b: fold the T1 (R_t, T_t) pairs of every MSM to its value
+//   V = sum_t R_t + s sum_t t T_t        (s = RED_J initially)
+// 8:1 per level: group g = {8g .. 8g+7} becomes
+//   R'_g = sum_i R_{8g+i} + s sum_i i T_{8g+i},   T'_g = sum_i T_{8g+i},
+// with s' = 8 s, which preserves V.  A 256-thread block folds 2048 / T1
+// MSMs in place in rt; at every level the live groups of all its MSMs are
+// packed onto the lowest threads so the shrinking levels occupy one
+// wavefront instead of one per MSM.  The thread of the last group converts
+// the MSM value to canonical affine (or stores the XYZZ point to xyzz_out
+// for chunked single MSMs, summed by k_xyzz_sum).
 template <class C>
-KZGX_DEV Xyzz<C> xyzz_shfl(const Xyzz<C>& p, int src) {
-  constexpr int L = C::Fp29::L;
-  Xyzz<C> r;
-#pragma unroll
-  for (int i = 0; i < L; i++) {
-    r.X.v[i] = __shfl(p.X.v[i], src, 64);
-    r.Y.v[i] = __shfl(p.Y.v[i], src, 64);
-    r.ZZ.v[i] = __shfl(p.ZZ.v[i], src, 64);
-    r.ZZZ.v[i] = __shfl(p.ZZZ.v[i], src, 64);
-  }
-  return r;
-}
-
-// pass 5b: one wavefront per MSM folds the T1 (R_t, T_t) pairs 4:1 per
-// level.  A level with scale s maps groups g = {4g..4g+3} to
-//   R'_g = sum_i R_{4g+i} + s (T_{4g+1} + 2 T_{4g+2} + 3 T_{4g+3}),
-//   T'_g = sum_i T_{4g+i},   scale' = 4 s,
-// which preserves  sum_t R_t + s sum_t t T_t.  When one pair is left, R is
-// the MSM value; lane 0 converts it to canonical affine, or stores the XYZZ
-// point to xyzz_out (chunked single MSMs, summed by k_xyzz_sum).
-template <class C>
-__global__ __launch_bounds__(256) void k_msm_window_tail(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
-                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
-                                                         uint32_t* __restrict__ xyzz_out) {
+__global__ __launch_bounds__(256) void k_msm_fold(uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
+                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                  uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= batch) return;  // whole wavefront
-  const uint32_t* src = rt + (size_t)b * T1 * 2 * XW;
-  uint32_t cnt = T1;  // pairs alive
-  uint32_t s = RED_J;
-  // first level straight from memory: groups of G = max(4, T1/64) pairs so
-  // that at most 64 groups remain (T1 is a power of two in [64, 512])
-  Xyzz<C> R = xyzz_inf<C>(), T = xyzz_inf<C>();
-  {
-    const uint32_t G = T1 / 64 > 4 ? T1 / 64 : 4;
-    const uint32_t groups = cnt / G;
-    if (lane < groups) {
-      const uint32_t* g0 = src + (size_t)lane * G * 2 * XW;
-      Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>(), r = xyzz_inf<C>();
-      for (int i = (int)G - 1; i >= 1; i--) {
-        u = xyzz_add<C>(u, xyzz_load<C>(g0 + (size_t)i * 2 * XW + XW));
-        v = xyzz_add<C>(v, u);  // v = sum_i i T_i
-        r = xyzz_add<C>(r, xyzz_load<C>(g0 + (size_t)i * 2 * XW));
-      }
-      for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
-      r = xyzz_add<C>(r, xyzz_load<C>(g0));
-      R = xyzz_add<C>(r, v);
-      T = xyzz_add<C>(xyzz_load<C>(g0 + XW), u);
-    }
-    cnt = groups;
-    s *= G;
-  }
-  // remaining levels inside the wavefront: lane g gathers lanes 4g..4g+3
+  const uint32_t mpb = 2048u / T1;  // MSMs per block (T1 in [64, 512])
+  const uint32_t tid = threadIdx.x;
+  uint32_t cnt = T1, stride = 1, s = RED_J;
   while (cnt > 1) {
-    const uint32_t gsz = cnt >= 4 ? 4 : cnt;
-    const uint32_t groups = cnt / gsz;
-    Xyzz<C> r4[4], t4[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int from = (int)(lane * gsz + i) & 63;
-      r4[i] = xyzz_shfl<C>(R, from);
-      t4[i] = xyzz_shfl<C>(T, from);
-    }
-    if (lane < groups) {
-      Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>();
-      for (int i = (int)gsz - 1; i >= 1; i--) {
-        u = xyzz_add<C>(u, t4[i]);
-        v = xyzz_add<C>(v, u);
+    const uint32_t G = cnt >= 8 ? 8 : cnt;
+    const uint32_t groups = cnt / G;
+    if (tid < groups * mpb) {
+      const uint32_t b = blockIdx.x * mpb + tid / groups;
+      const uint32_t g = tid % groups;
+      if (b < batch) {
+        uint32_t* base = rt + ((size_t)b * T1 + (size_t)g * G * stride) * 2 * XW;
+        const size_t step = (size_t)stride * 2 * XW;
+        Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>(), r = xyzz_inf<C>();
+        for (int i = (int)G - 1; i >= 1; i--) {
+          u = xyzz_add<C>(u, xyzz_load<C>(base + i * step + XW));
+          v = xyzz_add<C>(v, u);  // v = sum_i i T_i
+          r = xyzz_add<C>(r, xyzz_load<C>(base + i * step));
+        }
+        for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
+        r = xyzz_add<C>(r, xyzz_load<C>(base));
+        const Xyzz<C> R = xyzz_add<C>(r, v);
+        if (groups > 1) {
+          xyzz_store<C>(base, R);
+          xyzz_store<C>(base + XW, xyzz_add<C>(xyzz_load<C>(base + XW), u));
+        } else if (xyzz_out) {
+          xyzz_store<C>(xyzz_out + (size_t)b * XW, R);
+        } else {
+          Affine<C> a;
+          const bool fin = xyzz_to_affine<C>(R, a);
+          affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+          out_inf[b] = fin ? 0u : 1u;
+        }
       }
-      for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
-      Xyzz<C> r = r4[0];
-      for (uint32_t i = 1; i < gsz; i++) r = xyzz_add<C>(r, r4[i]);
-      R = xyzz_add<C>(r, v);
-      T = xyzz_add<C>(t4[0], u);
     }
+    __syncthreads();
     cnt = groups;
-    s *= gsz;
-  }
-  if (lane == 0) {
-    if (xyzz_out) {
-      xyzz_store<C>(xyzz_out + (size_t)b * XW, R);
-      return;
-    }
-    Affine<C> a;
-    bool fin = xyzz_to_affine<C>(R, a);
-    affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
-    out_inf[b] = fin ? 0u : 1u;
+    stride *= G;
+    s *= G;
   }
 }
 
@@ -461,6 +442,7 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, batch * NB * XB, &ws.bsum_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, batch * smax * XB, &ws.heads_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, batch * smax * XB, &ws.tails_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, batch * smax * 4, &ws.tailk_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / RED_J) * 2 * XB, &ws.rt_b));
   KZGX_TRY_HIP(hipMemsetAsync(ws.counts, 0, batch * NB * 4, st));
   dim3 blk(256);
@@ -483,14 +465,18 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     ProfScope p(ctx, st, "msm_accum");
     dim3 ga((unsigned)((smax + 255) / 256), (unsigned)batch);
     hipLaunchKernelGGL(k_msm_accum<C>, ga, blk, 0, st, ws.entries, emax, ws.offsets, NB, ctx->d_table, K, smax,
-                       ws.bsum, ws.heads, ws.tails);
+                       ws.bsum, ws.heads, ws.tails, ws.tailk);
   }
   {
     ProfScope p(ctx, st, "msm_reduce");
     const uint32_t T1 = NB / RED_J;
-    hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB, K,
-                       smax, ws.bsum, ws.heads, ws.tails, ws.rt);
-    hipLaunchKernelGGL(k_msm_window_tail<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
+    static_assert(NB / RED_J >= 64 && NB / RED_J <= 512, "k_msm_fold packs 2048 / T1 MSMs per block");
+    hipLaunchKernelGGL(k_msm_fixup<C>, dim3((unsigned)((smax + 255) / 256), (unsigned)batch), blk, 0, st, ws.offsets,
+                       NB, K, smax, ws.heads, ws.tails, ws.tailk, ws.bsum);
+    hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
+                       ws.bsum, ws.rt);
+    const uint32_t mpb = 2048u / T1;
+    hipLaunchKernelGGL(k_msm_fold<C>, dim3((unsigned)((batch + mpb - 1) / mpb)), blk, 0, st, ws.rt, T1,
                        (uint32_t)batch, d_out, d_out_inf, xyzz_out);
   }
   KZGX_TRY_HIP(hipGetLastError());

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libkzgx.so")
+LIB_PATH = os.environ.get("KZGX_LIB", os.path.join(PKG_DIR, "libkzgx.so"))
 CURVES = {"BN254": 0, "BLS12381": 1}
 BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 
