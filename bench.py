@@ -46,6 +46,12 @@ def parse():
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
+    ap.add_argument("--fixed-bits", type=int, default=-1,
+                    help="fixed-base table window (0 = Pippenger only; default 16 BN254 = 137.5 GB, "
+                         "15 BLS12-381 = 116 GB)")
+    ap.add_argument("--fixed-ppt", type=int, default=16, help="SRS points per accumulation thread (fixed-base path)")
+    ap.add_argument("--serial", action="store_true",
+                    help="commit and proof batches on one stream (exact per-kernel event timing)")
     ap.add_argument("--split", type=int, default=1, help="sub-batches (each on its own stream) per batch")
     ap.add_argument("--cpu-sample", type=int, default=3, help="commits (+ as many proofs) timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -111,6 +117,15 @@ def main():
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, 5000)
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (16 if curve == "BN254" else 15)
+    t_setup = time.perf_counter()
+    if fixed_bits:
+        # precompute the signed-digit multiples of the 4097-point SRS prefix
+        # (setup time, like the reference's trusted_setup ctor; not timed)
+        ctx.set_fixed_base(fixed_bits, n)
+        ctx.set_fixed_points_per_thread(args.fixed_ppt)
+    t_setup = time.perf_counter() - t_setup
+    fb = ctx.fixed_base_info()
     w64 = ctx.w64
 
     rng = np.random.default_rng(0x4B5A47 + rank)
@@ -136,6 +151,8 @@ def main():
     # (bucket sums, tails) of one overlap the accumulation of another
     S = max(1, args.split)
     streams = [torch.cuda.Stream(device=dev) for _ in range(2 * S)]
+    if args.serial:
+        streams = [streams[0]] * (2 * S)
     stream = streams[0]
     cstride = 0 if args.workload == "cfg3" else n
     cut = [B * s // S for s in range(S + 1)]
@@ -169,7 +186,8 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for s in streams[1:]:
-        s.wait_event(ev0)
+        if s is not stream:
+            s.wait_event(ev0)
     for _ in range(args.steps):
         step()
     for s in streams[1:]:
@@ -279,7 +297,11 @@ def main():
                 traffic = None
         total_units = units_per_step * args.steps * world
         value = total_units / elapsed
-        madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * ((257 + args.window_bits - 1) // args.window_bits)
+        if fb[0]:
+            wins = (C.r.bit_length() + 1 + fb[0] - 1) // fb[0]
+        else:
+            wins = (257 + args.window_bits - 1) // args.window_bits
+        madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * wins
         line = {
             "metric": "KZG commits/sec + proofs/sec, %s degree-4096" % curve,
             "value": value,
@@ -291,7 +313,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / (2.0 / (REF_COMMIT_S + REF_PROOF_S))) if args.workload == "cfg2" else None,
-            "dtype": "uint32 limbs (254-bit Montgomery Fp)" if curve == "BN254" else "uint32 limbs (381-bit Montgomery Fp)",
+            "dtype": "u32 (radix-2^29 Montgomery limbs, %d-bit Fp)" % (254 if curve == "BN254" else 381),
             "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 from fixed tau",
             "config": {
                 "workload": {"cfg2": "BN254 degree-4096 commit + single-opening proof, batched",
@@ -302,9 +324,10 @@ def main():
                 "batch_per_gpu": B,
                 "srs_points": 5000,
                 "parallelism": "dp%d (independent batches, no collective)" % world,
-                "window_bits": args.window_bits,
-                "segment": args.segment,
-                "streams": 2 * max(1, args.split),
+                "msm": ("fixed-base table, c=%d, %d windows, %.1f GB, %d points/thread" % (
+                    fb[0], wins, fb[2] / 1e9, args.fixed_ppt)) if fb[0] else
+                       ("pippenger, c=%d, segment %d" % (args.window_bits, args.segment)),
+                "streams": 1 if args.serial else 2 * max(1, args.split),
             },
             "roofline": {
                 "kernel": "msm_accum",
@@ -323,6 +346,7 @@ def main():
                 if acc_cnt else None,
                 "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
                 "event_ms_total": ev_ms,
+                "fixed_table_setup_s": t_setup if fb[0] else None,
             },
             "parity": {"checked": checked, "ok": int(ok), "method": "[P(tau)]G1 / [q(tau)]G1 identity"},
             "cpu_baseline": cpu,

@@ -81,6 +81,20 @@ int kzgx_prof_clear(kzgx_ctx* ctx);
 int kzgx_set_window_bits(kzgx_ctx* ctx, int c);
 int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
 
+/* fixed-base precomputation (the SRS is fixed for a trusted_setup's
+ * lifetime): store M[w][i][j] = (j+1) 2^(c w) SRS[i] for the first n_points
+ * SRS points, w < ceil((bits(r)+1)/c), j < 2^(c-1), packed affine
+ * (2 x 32 B BN254, 2 x 48 B BLS12-381).  Every MSM with n <= n_points then
+ * runs as a plain sum of table points (no bucket sort / reduction).  Built
+ * now if an SRS is installed, else when one is; rebuilt on every SRS change.
+ * c = 0 turns it off (Pippenger for every MSM).  c in {4, 8, 10, 12..16};
+ * BN254 c = 15 over 4097 points takes 73 GB of device memory. */
+int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
+/* built table: window bits (0 = none), points covered, device bytes */
+int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
+/* SRS points summed per accumulation thread on the fixed-base path (default 16) */
+int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p);
+
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */
 int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n);

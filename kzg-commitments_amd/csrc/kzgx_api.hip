@@ -133,8 +133,10 @@ void kzgx_destroy(kzgx_ctx* ctx) {
                   c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  kzgx::fixed_free(&c);
   for (auto& w : c.ws) {
-    void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum, w.heads, w.tails, w.tailk, w.rt, w.q, w.parts};
+    void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
+                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum};
     for (void* p : wb)
       if (p) (void)hipFree(p);
   }
@@ -205,6 +207,33 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k) {
   KZGX_TRY(activate(ctx));
   if (k < 1 || k > 4096) return KZGX_ERR_ARG;
   ctx->c.seg_k = k;
+  return KZGX_OK;
+}
+
+int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points) {
+  KZGX_TRY(activate(ctx));
+  if (!kzgx::fixed_bits_supported(c)) return KZGX_ERR_ARG;
+  if (c != 0 && n_points == 0) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  kzgx::fixed_free(&ctx->c);
+  ctx->c.fixed.c_req = c;
+  ctx->c.fixed.n_req = c ? n_points : 0;
+  if (c != 0 && ctx->c.n_srs != 0) KZGX_TRY(kzgx::fixed_build(&ctx->c, ctx->d_srs_canon, ctx->c.n_srs));
+  return KZGX_OK;
+}
+
+int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes) {
+  if (!ctx) return KZGX_ERR_ARG;
+  if (c) *c = ctx->c.fixed.c;
+  if (n_points) *n_points = ctx->c.fixed.n_t;
+  if (bytes) *bytes = ctx->c.fixed.bytes;
+  return KZGX_OK;
+}
+
+int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p) {
+  KZGX_TRY(activate(ctx));
+  if (p < 1 || p > 1024) return KZGX_ERR_ARG;
+  ctx->c.fixed.pts_per_thread = p;
   return KZGX_OK;
 }
 

@@ -39,14 +39,27 @@ int hip_fail(hipError_t e);
 struct MsmWs {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursors = nullptr, *entries = nullptr;
   uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr, *tailk = nullptr, *rt = nullptr, *q = nullptr,
-           *parts = nullptr;
+           *parts = nullptr, *fpart = nullptr, *fsum = nullptr;
   size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0, tailk_b = 0,
-         rt_b = 0, q_b = 0, parts_b = 0;
+         rt_b = 0, q_b = 0, parts_b = 0, fpart_b = 0, fsum_b = 0;
   hipStream_t owner = nullptr;  // workspaces are per stream so calls on
   bool used = false;            // different streams may run concurrently
 };
 
 constexpr int KZGX_MAX_STREAMS = 8;
+
+// precomputed signed-digit multiples of the SRS prefix (msm_fixed.hip):
+// M[w][i][j] = (j + 1) 2^(c w) P_i, packed affine, w < W, i < n_t, j < 2^(c-1)
+struct FixedTable {
+  int c_req = 0;        // requested window bits (0 = off)
+  size_t n_req = 0;     // requested SRS prefix length
+  uint32_t pts_per_thread = 16;
+  int c = 0, W = 0;     // built table
+  size_t n_t = 0;
+  uint32_t* d = nullptr;
+  size_t bytes = 0;
+  uint8_t* inf = nullptr;  // [n_t] infinite SRS points (skipped)
+};
 
 // optional per-kernel timing with HIP events on the launch stream
 struct ProfRec {
@@ -67,6 +80,7 @@ struct Ctx {
   uint8_t* d_inf = nullptr;  // [n_srs]
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];
+  FixedTable fixed;
   // the workspace bound to stream st (claimed on first use); nullptr when
   // more than KZGX_MAX_STREAMS distinct streams are used
   MsmWs* ws_for(hipStream_t st) {
@@ -116,6 +130,13 @@ struct ProfScope {
 int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap);
 
 bool window_bits_supported(int c);
+bool fixed_bits_supported(int c);
+int fixed_windows(int curve, int c);
+int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);
+void fixed_free(Ctx* ctx);
+bool fixed_usable(const Ctx* ctx, size_t n);
+int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+              uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out);
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st);

@@ -419,7 +419,7 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   hipLaunchKernelGGL(k_table_build<C>, grd, blk, 0, ctx->stream, ctx->d_table, ctx->d_inf, (uint32_t)n, W, ctx->c);
   KZGX_TRY_HIP(hipGetLastError());
   ctx->n_srs = n;
-  return KZGX_OK;
+  return fixed_build(ctx, d_canon, n);
 }
 
 template <class C, int CB>
@@ -539,6 +539,7 @@ static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uin
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;
+  if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
   if (batch == 1 && n >= 4 * MSM_CHUNK)
     return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
               : msm_single_chunked<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);

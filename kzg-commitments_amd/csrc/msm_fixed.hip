@@ -1,0 +1,448 @@
+// Fixed-base G1 MSM with a precomputed table of signed-digit multiples
+// (Brickell-Gordon-McCurley-Wilson style) for gfx950 -- the fast path behind
+// kzg::trusted_setup::create_commit / create_proof / verify_commit when the
+// SRS prefix is small enough to precompute
+// (reference: trusted_setup::polyeval_G1, src/trusted_setup.cpp:149-174, a
+// naive per-term PAIR_G1mul + ECP_add loop).
+//
+// The SRS is fixed for the lifetime of a trusted_setup, so the work that
+// does not depend on the scalars is paid once, at setup time:
+//
+//   M[w][i][j] = (j + 1) 2^(c w) P_i      w < W, i < n_t, j < H = 2^(c-1)
+//
+// stored affine, Montgomery form, packed to 2 x 32 B (BN254) / 2 x 48 B
+// (BLS12-381).  A scalar s_i with signed c-bit digits d_w (|d_w| <= H) then
+// contributes sum_w sign(d_w) M[w][i][|d_w| - 1], so an MSM is a plain sum
+// of n W table points: no bucket sort, no bucket reduction, no doublings.
+// Each thread sums the W terms of ~P points into one XYZZ accumulator with
+// mixed additions (the only heavy instruction stream: 8M + 2S per term, the
+// table lookup for the next term in flight underneath), one wavefront per
+// MSM folds the partials, and one thread per MSM converts to affine.
+//
+// Size: W n_t H points; BN254 c = 15 (W = 17) for the 4097-point prefix of
+// the degree-4096 benchmark is 73 GB -- sized for the 288 GB of HBM3E.
+// Every step is an exact group operation, so the affine output is bit-exact
+// with any other correct evaluation of sum c_i [tau^i]G1.
+#include <hip/hip_runtime.h>
+
+#include "curve.hpp"
+#include "kzgx_internal.hpp"
+
+namespace kzgx {
+
+// packed table point: x || y as NW-word little-endian Montgomery residues < m
+template <class C>
+constexpr int packed_words() {
+  return 2 * C::Fp::N;
+}
+
+template <class C, int CB>
+struct FixedWin {
+  // signed digits of a scalar < r need W c >= bits(r) + 1: the top digit
+  // then absorbs the final carry without overflowing H
+  static constexpr int W = (C::SCALAR_BITS + 1 + CB - 1) / CB;
+  static constexpr uint32_t H = 1u << (CB - 1);
+};
+
+int fixed_windows(int curve, int c) {
+  const int bits = curve == KZGX_CURVE_BN254 ? BN254G1::SCALAR_BITS : BLS12381G1::SCALAR_BITS;
+  return (bits + 1 + c - 1) / c;
+}
+
+template <class C>
+KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+#pragma unroll
+  for (int k = 0; k < N / 4; k++) {
+    uint4 a = reinterpret_cast<const uint4*>(p)[k];
+    uint4 b = reinterpret_cast<const uint4*>(p + N)[k];
+    wx[4 * k] = a.x; wx[4 * k + 1] = a.y; wx[4 * k + 2] = a.z; wx[4 * k + 3] = a.w;
+    wy[4 * k] = b.x; wy[4 * k + 1] = b.y; wy[4 * k + 2] = b.z; wy[4 * k + 3] = b.w;
+  }
+  Affine<C> r;
+  r.x = f29_from_words<F, N>(wx);
+  r.y = f29_from_words<F, N>(wy);
+  return r;
+}
+
+template <class C>
+KZGX_DEV void packed_store(uint32_t* __restrict__ p, const Affine<C>& a) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  f29_to_words<F, N>(a.x, wx);
+  f29_to_words<F, N>(a.y, wy);
+#pragma unroll
+  for (int k = 0; k < N / 4; k++) {
+    reinterpret_cast<uint4*>(p)[k] = make_uint4(wx[4 * k], wx[4 * k + 1], wx[4 * k + 2], wx[4 * k + 3]);
+    reinterpret_cast<uint4*>(p + N)[k] = make_uint4(wy[4 * k], wy[4 * k + 1], wy[4 * k + 2], wy[4 * k + 3]);
+  }
+}
+
+// s mod r for any 256-bit s (the ABI asks for canonical scalars; this keeps a
+// non-canonical one exact for points of order r instead of overflowing the
+// top digit).  Common case: one compare of the top word.
+template <class C>
+KZGX_DEV void scalar_reduce(uint32_t (&s)[8]) {
+  using R = typename C::Fr;
+  while (s[7] >= R::P[7]) {
+    uint32_t d[8];
+    int64_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      int64_t v = (int64_t)s[k] - (int64_t)R::P[k] + br;
+      d[k] = (uint32_t)v;
+      br = v >> 32;
+    }
+    if (br < 0) break;  // s < r
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = d[k];
+  }
+}
+
+// --------------------------------------------------------------------------
+// table construction (setup time)
+// --------------------------------------------------------------------------
+// window bases B[w][i] = 2^(c w) P_i, packed; thread per SRS point
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_bases(const uint32_t* __restrict__ canon, uint32_t n, int W, int c,
+                                                    uint32_t* __restrict__ bases, uint8_t* __restrict__ inf) {
+  constexpr int PW = packed_words<C>();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<C> a;
+  const bool finite = affine_from_canonical<C>(canon + (size_t)i * 2 * C::Fp::N, a);
+  inf[i] = finite ? 0 : 1;
+  for (int w = 0; w < W; w++) {
+    packed_store<C>(bases + ((size_t)w * n + i) * PW, a);
+    if (finite && w + 1 < W) {
+      Xyzz<C> p = xyzz_from_affine<C>(a);
+      for (int s = 0; s < c; s++) p = xyzz_dbl<C>(p);
+      xyzz_to_affine<C>(p, a);  // 2^(cw) P_i != O: P_i has order r > 2^(cw)
+    }
+  }
+}
+
+// M[w][i][j0 + j] = (j0 + j + 1) B[w][i], j < J; thread per (w, i, block)
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restrict__ bases,
+                                                        const uint8_t* __restrict__ inf, uint32_t n, int W, uint32_t H,
+                                                        uint32_t J, uint64_t g0, uint64_t cnt,
+                                                        uint32_t* __restrict__ tab) {
+  constexpr int PW = packed_words<C>();
+  const uint64_t gl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nblk = H / J;
+  if (gl >= cnt) return;
+  const uint64_t g = g0 + gl;  // < W n nblk
+  const uint32_t blk = (uint32_t)(g % nblk);
+  const uint64_t wi = g / nblk;  // w * n + i
+  const uint32_t i = (uint32_t)(wi % n);
+  uint32_t* out = tab + (wi * H + (uint64_t)blk * J) * PW;
+  if (inf[i]) {  // never read: the MSM skips infinite SRS points
+    for (uint32_t j = 0; j < J * PW; j++) out[j] = 0;
+    return;
+  }
+  const Affine<C> B = packed_load<C>(bases + wi * PW);
+  const uint32_t k0 = blk * J + 1;
+  // acc = k0 B, left-to-right double-and-add
+  Xyzz<C> acc = xyzz_from_affine<C>(B);
+  for (int bit = 30 - __builtin_clz(k0) ; bit >= 0; bit--) {
+    acc = xyzz_dbl<C>(acc);
+    if ((k0 >> bit) & 1u) acc = xyzz_add_affine<C>(acc, B);
+  }
+  for (uint32_t j = 0; j < J; j++) {
+    if (j) acc = xyzz_add_affine<C>(acc, B);
+    Affine<C> a;
+    xyzz_to_affine<C>(acc, a);  // (k0 + j) B != O since k0 + j <= H < r
+    packed_store<C>(out + (size_t)j * PW, a);
+  }
+}
+
+// --------------------------------------------------------------------------
+// MSM
+// --------------------------------------------------------------------------
+// shift the 256-bit scalar right by CB (static register indexing only)
+template <int CB>
+KZGX_DEV void shr_scalar(uint32_t (&s)[8]) {
+#pragma unroll
+  for (int k = 0; k < 7; k++) s[k] = __builtin_amdgcn_alignbit(s[k + 1], s[k], CB);
+  s[7] >>= CB;
+}
+
+// next signed digit from the low CB bits of s (consumed), carry in/out
+template <int CB>
+KZGX_DEV int next_digit(uint32_t (&s)[8], uint32_t& carry) {
+  uint32_t raw = (s[0] & ((1u << CB) - 1u)) + carry;
+  shr_scalar<CB>(s);
+  carry = raw > (1u << (CB - 1)) ? 1u : 0u;
+  return (int)raw - (int)(carry << CB);
+}
+
+// thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
+// (a wavefront reads 64 consecutive scalars per point step)
+template <class C>
+struct PackedPt {
+  uint4 q[packed_words<C>() / 4];
+};
+
+template <class C>
+KZGX_DEV PackedPt<C> packed_fetch(const uint32_t* __restrict__ p) {
+  PackedPt<C> r;
+#pragma unroll
+  for (int k = 0; k < packed_words<C>() / 4; k++) r.q[k] = reinterpret_cast<const uint4*>(p)[k];
+  return r;
+}
+
+template <class C>
+KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+#pragma unroll
+  for (int k = 0; k < N / 4; k++) {
+    const uint4 a = r.q[k], b = r.q[N / 4 + k];
+    wx[4 * k] = a.x; wx[4 * k + 1] = a.y; wx[4 * k + 2] = a.z; wx[4 * k + 3] = a.w;
+    wy[4 * k] = b.x; wy[4 * k + 1] = b.y; wy[4 * k + 2] = b.z; wy[4 * k + 3] = b.w;
+  }
+  Affine<C> a;
+  a.x = f29_from_words<F, N>(wx);
+  a.y = f29_from_words<F, N>(wy);
+  return a;
+}
+
+// waves per SIMD the accumulation kernel is register-budgeted for
+template <class C>
+constexpr int fixed_accum_waves() {
+  return C::Fp29::L <= 9 ? 3 : 2;
+}
+
+// thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
+// (a wavefront reads 64 consecutive scalars per point step)
+template <class C, int CB>
+__global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
+    const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
+    uint32_t n_t, const uint8_t* __restrict__ inf, uint32_t T, uint32_t* __restrict__ part) {
+  constexpr int PW = packed_words<C>();
+  constexpr int XW = xyzz_words<C>();
+  constexpr int W = FixedWin<C, CB>::W;
+  constexpr uint32_t H = FixedWin<C, CB>::H;
+  const uint32_t b = blockIdx.y;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const uint32_t* sc = scalars + (size_t)b * stride_words;
+  const size_t wstride = (size_t)n_t * H * PW;  // words between windows
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t i = t; i < n; i += T) {
+    if (inf[i]) continue;
+    uint32_t s[8];
+    {
+      uint4 lo = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[0];
+      uint4 hi = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[1];
+      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
+      s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+    }
+    scalar_reduce<C>(s);
+    const uint32_t* base = tab + (size_t)i * H * PW;
+    uint32_t carry = 0;
+    // software pipeline: the (packed) lookup of term w + 1 is in flight
+    // during the mixed addition of term w
+    int d = next_digit<CB>(s, carry);
+    PackedPt<C> nx = packed_fetch<C>(base + (size_t)((d < 0 ? -d : d) - (d != 0)) * PW);
+#pragma unroll 1
+    for (int w = 0; w < W; w++) {
+      Affine<C> cur = packed_unpack<C>(nx);
+      int dn = 0;
+      if (w + 1 < W) {
+        dn = next_digit<CB>(s, carry);
+        nx = packed_fetch<C>(base + (size_t)(w + 1) * wstride + (size_t)((dn < 0 ? -dn : dn) - (dn != 0)) * PW);
+      }
+      if (d != 0) {
+        if (d < 0) cur = affine_neg<C>(cur);
+        acc = xyzz_add_affine_impl<C>(acc, cur);
+      }
+      d = dn;
+    }
+  }
+  xyzz_store<C>(part + ((size_t)b * T + t) * XW, acc);
+}
+
+// one wavefront per MSM: strided sums of the T partials, then a shuffle tree
+template <class C>
+__global__ __launch_bounds__(256) void k_fixed_reduce(const uint32_t* __restrict__ part, uint32_t T, uint32_t batch,
+                                                      uint32_t* __restrict__ sums) {
+  constexpr int XW = xyzz_words<C>();
+  constexpr int L = C::Fp29::L;
+  const uint32_t b = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  if (b >= batch) return;  // whole wavefronts
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t k = lane; k < T; k += 64) acc = xyzz_add<C>(acc, xyzz_load<C>(part + ((size_t)b * T + k) * XW));
+  for (int off = 32; off >= 1; off >>= 1) {
+    Xyzz<C> o;
+#pragma unroll
+    for (int k = 0; k < L; k++) {
+      o.X.v[k] = __shfl_down(acc.X.v[k], off, 64);
+      o.Y.v[k] = __shfl_down(acc.Y.v[k], off, 64);
+      o.ZZ.v[k] = __shfl_down(acc.ZZ.v[k], off, 64);
+      o.ZZZ.v[k] = __shfl_down(acc.ZZZ.v[k], off, 64);
+    }
+    acc = xyzz_add<C>(acc, o);
+  }
+  if (lane == 0) xyzz_store<C>(sums + (size_t)b * XW, acc);
+}
+
+// thread per MSM: XYZZ -> canonical affine + infinity flag, or copy the XYZZ
+// point out (chunked callers sum partials themselves)
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_finish(const uint32_t* __restrict__ sums, uint32_t batch,
+                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                     uint32_t* __restrict__ xyzz_out) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const Xyzz<C> p = xyzz_load<C>(sums + (size_t)b * XW);
+  if (xyzz_out) {
+    xyzz_store<C>(xyzz_out + (size_t)b * XW, p);
+    return;
+  }
+  Affine<C> a;
+  const bool fin = xyzz_to_affine<C>(p, a);
+  affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+  out_inf[b] = fin ? 0u : 1u;
+}
+
+// --------------------------------------------------------------------------
+// host side
+// --------------------------------------------------------------------------
+constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
+
+template <class C>
+static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
+  FixedTable& ft = ctx->fixed;
+  const int c = ft.c_req;
+  const int W = fixed_windows(ctx->curve, c);
+  const uint64_t H = 1ull << (c - 1);
+  const size_t PB = packed_words<C>() * sizeof(uint32_t);
+  const size_t bytes = (size_t)W * n * H * PB;
+  // drop the old table first: the new one may need most of the device
+  if (ft.d) {
+    KZGX_TRY_HIP(hipDeviceSynchronize());
+    KZGX_TRY_HIP(hipFree(ft.d));
+    ft.d = nullptr;
+    ft.bytes = 0;
+  }
+  ft.n_t = 0;
+  KZGX_TRY_HIP(hipMalloc((void**)&ft.d, bytes));
+  ft.bytes = bytes;
+  uint32_t* d_bases = nullptr;
+  uint8_t* d_inf = nullptr;
+  KZGX_TRY_HIP(hipMalloc((void**)&d_bases, (size_t)W * n * PB));
+  KZGX_TRY_HIP(hipMalloc((void**)&d_inf, n));
+  hipStream_t st = ctx->stream;
+  hipLaunchKernelGGL(k_fixed_bases<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_canon, (uint32_t)n, W, c,
+                     d_bases, d_inf);
+  const uint32_t J = (uint32_t)(H < FIXED_J ? H : FIXED_J);
+  const uint64_t tasks = (uint64_t)W * n * (H / J);
+  // bounded launches of <= 2^22 threads each, synchronised per slice so one
+  // setup never queues seconds of work behind a single dispatch
+  const uint64_t slice = 1ull << 22;
+  for (uint64_t s0 = 0; s0 < tasks; s0 += slice) {
+    const uint64_t cnt = tasks - s0 < slice ? tasks - s0 : slice;
+    {
+      ProfScope p(ctx, st, "fixed_build");
+      hipLaunchKernelGGL(k_fixed_multiples<C>, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, d_bases, d_inf,
+                         (uint32_t)n, W, (uint32_t)H, J, s0, cnt, ft.d);
+    }
+    KZGX_TRY_HIP(hipGetLastError());
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+  }
+  (void)hipFree(d_bases);
+  ft.inf = d_inf;
+  ft.c = c;
+  ft.W = W;
+  ft.n_t = n;
+  return KZGX_OK;
+}
+
+int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
+  FixedTable& ft = ctx->fixed;
+  if (ft.c_req == 0 || ft.n_req == 0) return KZGX_OK;
+  const size_t n = ft.n_req < n_srs ? ft.n_req : n_srs;
+  return ctx->curve == KZGX_CURVE_BN254 ? fixed_build_impl<BN254G1>(ctx, d_canon, n)
+                                        : fixed_build_impl<BLS12381G1>(ctx, d_canon, n);
+}
+
+void fixed_free(Ctx* ctx) {
+  FixedTable& ft = ctx->fixed;
+  if (ft.d) (void)hipFree(ft.d);
+  if (ft.inf) (void)hipFree(ft.inf);
+  ft.d = nullptr;
+  ft.inf = nullptr;
+  ft.bytes = 0;
+  ft.n_t = 0;
+  ft.c = 0;
+}
+
+template <class C, int CB>
+static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                          uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  FixedTable& ft = ctx->fixed;
+  const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+  const uint32_t P0 = ft.pts_per_thread;
+  const uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
+  MsmWs* wsp = ctx->ws_for(st);
+  if (!wsp) return KZGX_ERR_ARG;
+  MsmWs& ws = *wsp;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * T * XB, &ws.fpart_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * XB, &ws.fsum_b));
+  {
+    ProfScope p(ctx, st, "msm_accum");
+    hipLaunchKernelGGL((k_fixed_accum<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
+                       (uint32_t)n, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, T, ws.fpart);
+  }
+  {
+    ProfScope p(ctx, st, "msm_reduce");
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, ws.fpart, T,
+                       (uint32_t)batch, ws.fsum);
+    hipLaunchKernelGGL(k_fixed_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, ws.fsum,
+                       (uint32_t)batch, d_out, d_out_inf, xyzz_out);
+  }
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+template <class C>
+static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  switch (ctx->fixed.c) {
+#define KZGX_FIXED_CASE(cb) \
+  case cb: return fixed_msm_impl<C, cb>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
+    KZGX_FIXED_CASE(4)
+    KZGX_FIXED_CASE(8)
+    KZGX_FIXED_CASE(10)
+    KZGX_FIXED_CASE(12)
+    KZGX_FIXED_CASE(13)
+    KZGX_FIXED_CASE(14)
+    KZGX_FIXED_CASE(15)
+    KZGX_FIXED_CASE(16)
+#undef KZGX_FIXED_CASE
+    default: return KZGX_ERR_INTERNAL;
+  }
+}
+
+bool fixed_bits_supported(int c) {
+  return c == 0 || c == 4 || c == 8 || c == 10 || (c >= 12 && c <= 16);
+}
+
+bool fixed_usable(const Ctx* ctx, size_t n) { return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t; }
+
+int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+              uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  return ctx->curve == KZGX_CURVE_BN254
+             ? fixed_msm_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out)
+             : fixed_msm_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
+}
+
+}  // namespace kzgx

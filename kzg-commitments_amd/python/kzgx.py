@@ -21,7 +21,8 @@ BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 # exported C symbols (must match include/kzg_gpu.h)
 EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
-    "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
+    "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_set_fixed_points_per_thread", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
@@ -60,6 +61,9 @@ def lib():
             "kzgx_prof_clear": (ctypes.c_int, [vp]),
             "kzgx_set_window_bits": (ctypes.c_int, [vp, ctypes.c_int]),
             "kzgx_set_segment": (ctypes.c_int, [vp, ctypes.c_uint]),
+            "kzgx_set_fixed_base": (ctypes.c_int, [vp, ctypes.c_int, sz]),
+            "kzgx_fixed_base_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+            "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_gen_srs_g1": (ctypes.c_int, [vp, u64p, sz, sz]),
             "kzgx_get_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
@@ -139,6 +143,22 @@ class Context:
 
     def set_segment(self, k: int):
         _chk(lib().kzgx_set_segment(self.h, k), "kzgx_set_segment")
+
+    def set_fixed_base(self, c: int, n_points: int = 0):
+        """Precompute the signed-digit multiples table for the first n_points
+        SRS points (c = 0: off).  Built now if an SRS is installed."""
+        _chk(lib().kzgx_set_fixed_base(self.h, c, n_points), "kzgx_set_fixed_base")
+
+    def fixed_base_info(self):
+        c = ctypes.c_int(0)
+        n = sz(0)
+        b = sz(0)
+        _chk(lib().kzgx_fixed_base_info(self.h, ctypes.byref(c), ctypes.byref(n), ctypes.byref(b)),
+             "kzgx_fixed_base_info")
+        return c.value, n.value, b.value
+
+    def set_fixed_points_per_thread(self, p: int):
+        _chk(lib().kzgx_set_fixed_points_per_thread(self.h, p), "kzgx_set_fixed_points_per_thread")
 
     def prof_clear(self):
         _chk(lib().kzgx_prof_clear(self.h), "kzgx_prof_clear")

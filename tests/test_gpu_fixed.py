@@ -1,0 +1,172 @@
+"""GPU parity of the fixed-base (precomputed multiples) MSM path.
+
+kzgx_set_fixed_base precomputes M[w][i][j] = (j+1) 2^(c w) SRS[i]; MSMs over
+the covered SRS prefix then run as plain table sums (msm_fixed.hip).  Every
+result is checked bit-exactly against the CPU oracle: the naive per-term MSM
+of the reference's polyeval_G1 (src/trusted_setup.cpp:149-174) at small
+sizes, the MSM-independent identity commit == [P(tau)]G1 at full size.
+
+These tests make their own contexts (the table is per context and large)."""
+import numpy as np
+import pytest
+
+import kzg_ref as K
+
+pytestmark = pytest.mark.gpu
+
+CURVES = [("BN254", K.BN254), ("BLS12381", K.BLS12381)]
+
+
+def limbs(vals, nl=4):
+    import corc
+    return corc.ints_to_limbs(vals, nl)
+
+
+def pt(curve, row, inf=False):
+    import corc
+    return None if inf else corc.array_to_points(curve, row[None, :])[0]
+
+
+@pytest.fixture
+def fresh_ctx():
+    import kzgx
+    made = []
+
+    def get(curve):
+        c = kzgx.Context(curve)
+        made.append(c)
+        return c
+
+    yield get
+    for c in made:
+        c.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("c", [4, 8, 10, 12])
+def test_fixed_msm_matches_naive(name, C, c, fresh_ctx, oracle_c):
+    ctx = fresh_ctx(name)
+    n = 300
+    srs = oracle_c.gen_srs(name, K.default_tau(C), n)
+    ctx.load_srs(srs)
+    ctx.set_fixed_base(c, n)
+    cc, nt, nbytes = ctx.fixed_base_info()
+    assert (cc, nt) == (c, n) and nbytes > 0
+    sc = K.random_scalars(C, n, seed=31 + c)
+    # digit edge cases: zero, one, r - 1, every digit = +-H boundary, top window carries
+    H = 1 << (c - 1)
+    sc[0], sc[1], sc[2] = 0, 1, C.r - 1
+    sc[3] = sum(H << (c * w) for w in range(250 // c)) % C.r
+    sc[4] = (1 << 253) - 1
+    sc[5] = sum((H + 1) << (c * w) for w in range(250 // c)) % C.r
+    S = limbs(sc)
+    for n_use in (n, 1, 2, 65, 257):
+        out, inf = ctx.msm(S[:n_use])
+        assert pt(name, out, inf) == oracle_c.msm_naive(name, srs[:n_use], S[:n_use]), n_use
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_fixed_noncanonical_scalars(name, C, fresh_ctx, oracle_c):
+    """Scalars >= r (outside the ABI contract) still give s P = (s mod r) P."""
+    ctx = fresh_ctx(name)
+    n = 40
+    srs = oracle_c.gen_srs(name, K.default_tau(C), n)
+    ctx.load_srs(srs)
+    ctx.set_fixed_base(8, n)
+    sc = [C.r, C.r + 5, (1 << 256) - 1, 2 * C.r + 1] + K.random_scalars(C, n - 4, seed=9)
+    S = limbs(sc)
+    out, inf = ctx.msm(S)
+    assert pt(name, out, inf) == K.commit_via_tau(C, K.default_tau(C), [v % C.r for v in sc])
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("tau", [0, 1, 2, -1])
+def test_fixed_degenerate_srs(name, C, tau, fresh_ctx, oracle_c):
+    """tau = 0: infinite SRS points (skipped); tau = +-1: repeated points, so
+    the accumulator meets P == Q (doubling) and P == -Q (cancellation)."""
+    ctx = fresh_ctx(name)
+    t = tau % C.r
+    n = 200
+    srs = oracle_c.gen_srs(name, t, n)
+    ctx.load_srs(srs)
+    ctx.set_fixed_base(8, n)
+    sc = K.random_scalars(C, n, seed=5)
+    sc[7] = sc[3]
+    sc[9] = (C.r - sc[3]) % C.r
+    out, inf = ctx.msm(limbs(sc))
+    assert pt(name, out, inf) == K.commit_via_tau(C, t, sc)
+    # a sum that cancels exactly: s P_0 + (r - s) P_0 style via repeated points
+    if tau in (1, -1):
+        z = [0] * n
+        z[0], z[1] = 12345, (C.r - 12345) if tau == 1 else 12345
+        out, inf = ctx.msm(limbs(z))
+        assert inf and pt(name, out, inf) is None
+
+
+@pytest.mark.parametrize("ppt", [1, 3, 8, 64])
+def test_fixed_points_per_thread(ppt, fresh_ctx, oracle_c):
+    name, C = CURVES[0]
+    ctx = fresh_ctx(name)
+    n = 700
+    srs = oracle_c.gen_srs(name, K.default_tau(C), n)
+    ctx.load_srs(srs)
+    ctx.set_fixed_base(10, n)
+    ctx.set_fixed_points_per_thread(ppt)
+    sc = K.random_scalars(C, n, seed=ppt)
+    S = limbs(sc)
+    out, inf = ctx.msm(S)
+    assert pt(name, out, inf) == oracle_c.msm_naive(name, srs, S)
+
+
+def test_fixed_coverage_and_fallback(fresh_ctx, oracle_c):
+    """MSMs longer than the table fall back to Pippenger; the table follows
+    SRS changes; c = 0 turns it off."""
+    name, C = CURVES[0]
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C)
+    srs = oracle_c.gen_srs(name, tau, 500)
+    ctx.load_srs(srs)
+    ctx.set_fixed_base(8, 300)
+    assert ctx.fixed_base_info()[1] == 300
+    sc = K.random_scalars(C, 500, seed=3)
+    S = limbs(sc)
+    for n_use in (300, 301, 500):
+        out, inf = ctx.msm(S[:n_use])
+        assert pt(name, out, inf) == oracle_c.msm_naive(name, srs[:n_use], S[:n_use]), n_use
+    # a new SRS rebuilds the table (clamped to the SRS size)
+    ctx.gen_srs(tau + 1, 200)
+    c, nt, _ = ctx.fixed_base_info()
+    assert (c, nt) == (8, 200)
+    out, inf = ctx.msm(S[:200])
+    assert pt(name, out, inf) == K.commit_via_tau(C, tau + 1, sc[:200])
+    ctx.set_fixed_base(0)
+    assert ctx.fixed_base_info() == (0, 0, 0)
+    out, inf = ctx.msm(S[:200])
+    assert pt(name, out, inf) == K.commit_via_tau(C, tau + 1, sc[:200])
+    with pytest.raises(Exception):
+        ctx.set_fixed_base(7, 100)  # unsupported window
+    with pytest.raises(Exception):
+        ctx.set_fixed_base(8, 0)
+
+
+@pytest.mark.parametrize("name,C,c", [("BN254", K.BN254, 13), ("BLS12381", K.BLS12381, 12)])
+def test_fixed_degree4096_batch(name, C, c, fresh_ctx):
+    """BASELINE configs[1]/[3] size: degree-4096 commits and single-opening
+    proofs on the fixed-base path, against [P(tau)]G1 / [q(tau)]G1."""
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C)
+    n, batch = 4097, 5
+    ctx.gen_srs(tau, 5000)
+    ctx.set_fixed_base(c, n)
+    polys = [K.random_scalars(C, n, seed=177 + b) for b in range(batch)]
+    polys[1] = [0] * n
+    polys[2] = [5] + [0] * (n - 1)
+    S = np.concatenate([limbs(p) for p in polys])
+    out, inf = ctx.msm_batch(S, n, batch)
+    for b in range(batch):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+    zs = [0, 1, 7, C.r - 1]
+    pout, pinf, _ = ctx.prove_single_batch(limbs(polys[0]), limbs(zs))
+    for j, z in enumerate(zs):
+        q = K.proof_quotient(C, polys[0], z, 1)
+        assert pt(name, pout[j], pinf[j]) == K.commit_via_tau(C, tau, q), z
