@@ -87,7 +87,7 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
  * (2 x 32 B BN254, 2 x 48 B BLS12-381).  Every MSM with n <= n_points then
  * runs as a plain sum of table points (no bucket sort / reduction).  Built
  * now if an SRS is installed, else when one is; rebuilt on every SRS change.
- * c = 0 turns it off (Pippenger for every MSM).  c in {4, 8, 10, 12..16};
+ * c = 0 turns it off (Pippenger for every MSM).  c in {4, 8, 10, 12..17};
  * BN254 c = 15 over 4097 points takes 73 GB of device memory. */
 int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
 /* built table: window bits (0 = none), points covered, device bytes */

@@ -427,13 +427,14 @@ static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t bat
     KZGX_FIXED_CASE(14)
     KZGX_FIXED_CASE(15)
     KZGX_FIXED_CASE(16)
+    KZGX_FIXED_CASE(17)
 #undef KZGX_FIXED_CASE
     default: return KZGX_ERR_INTERNAL;
   }
 }
 
 bool fixed_bits_supported(int c) {
-  return c == 0 || c == 4 || c == 8 || c == 10 || (c >= 12 && c <= 16);
+  return c == 0 || c == 4 || c == 8 || c == 10 || (c >= 12 && c <= 17);
 }
 
 bool fixed_usable(const Ctx* ctx, size_t n) { return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t; }
