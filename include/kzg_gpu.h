@@ -151,6 +151,36 @@ int kzgx_g1_validate(kzgx_ctx* ctx, const uint64_t* xy, int* ok);
 /* out = sum of count affine points (is_inf may be NULL); host pointers */
 int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy, int* out_is_inf);
 
+/* ---- verify half: G2 setup, polyeval_G2, pairing ----------------------------
+ * G2 points are canonical affine on the sextic twist (BN254: D-type
+ * y^2 = x^3 + 2/(1+i); BLS12-381: M-type y^2 = x^3 + 4(1+i)), Fp2 = Fp[i],
+ * i^2 = -1, stored as x.re || x.im || y.re || y.im (4 x W64 limbs); all zero
+ * = infinity.  Fp12 values are 12 canonical Fp elements in tower order
+ * (Fp6 = Fp2[v]/(v^3 - (1+i)), Fp12 = Fp6[w]/(w^2 - v)):
+ * c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, each (re, im). */
+/* generate [tau^(start+i)] G2, i < n (G2 half of generate_elements_range,
+ * src/trusted_setup.cpp:123-135) and install it */
+int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n);
+/* install n canonical affine G2 points (G2 half of the setup-file loader,
+ * src/trusted_setup.cpp:103-118) */
+int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n);
+int kzgx_get_srs_g2(kzgx_ctx* ctx, uint64_t* xy, size_t n);
+size_t kzgx_srs_g2_size(const kzgx_ctx* ctx);
+/* ok[k] = 1 iff point k is canonical and on the twist (ECP2_fromOctet) */
+int kzgx_g2_validate(kzgx_ctx* ctx, const uint64_t* xy, size_t count, int* ok);
+/* out = sum_{i<n} scalars[i] [tau^i]G2 (polyeval_G2, src/trusted_setup.cpp:176-201) */
+int kzgx_msm_g2(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out_xy, int* out_is_inf);
+/* out[k] = e(P_k, Q_k): optimal ate pairing + final exponentiation
+ * (miracl PAIR_ate + PAIR_fexp, src/trusted_setup.cpp:240-250); inf flags may be NULL */
+int kzgx_pairing(kzgx_ctx* ctx, const uint64_t* g1_xy, const int* g1_inf, const uint64_t* g2_xy, const int* g2_inf,
+                 size_t count, uint64_t* out);
+/* trusted_setup::verify_proof (src/trusted_setup.cpp:230-254): *ok =
+ * e(proof, [Z(tau)]G2) == e(C - [I(tau)]G1, G2[0]) for the npoints opened
+ * points (xs, ys); npoints >= |SRS G1| gives *ok = 0; npoints == 0 is
+ * KZGX_ERR_ARG; needs a G2 setup of >= npoints + 1 points. */
+int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, const uint64_t* proof_xy,
+                      int proof_inf, const uint64_t* xs, const uint64_t* ys, size_t npoints, int* ok);
+
 #ifdef __cplusplus
 }
 #endif

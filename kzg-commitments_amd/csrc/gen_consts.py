@@ -87,6 +87,163 @@ def mont29(v, m, L):
     return v * (1 << (29 * L)) % m
 
 
+# --------------------------------------------------------------------------
+# G2 / pairing constants (verify path: trusted_setup.cpp:123-135, 176-201,
+# 230-254).  Fp2 = Fp[i]/(i^2+1), xi = 1 + i, Fp6 = Fp2[v]/(v^3 - xi),
+# Fp12 = Fp6[w]/(w^2 - v).  The twist type is selected by group order: the
+# sextic twist whose order is divisible by r (BN254: D-type y^2 = x^3 + b/xi,
+# BLS12-381: M-type y^2 = x^3 + b xi).
+# --------------------------------------------------------------------------
+def _f2mul(p, a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % p, (a[0] * b[1] + a[1] * b[0]) % p)
+
+
+def _f2pow(p, a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = _f2mul(p, r, a)
+        a = _f2mul(p, a, a)
+        e >>= 1
+    return r
+
+
+def _f2inv(p, a):
+    ni = pow((a[0] * a[0] + a[1] * a[1]) % p, -1, p)
+    return (a[0] * ni % p, (-a[1]) * ni % p)
+
+
+def _f2add(p, a, b):
+    return ((a[0] + b[0]) % p, (a[1] + b[1]) % p)
+
+
+def _f2sqrt(p, a):
+    a1 = _f2pow(p, a, (p - 3) // 4)
+    alpha = _f2mul(p, _f2mul(p, a1, a1), a)
+    if _f2mul(p, _f2pow(p, alpha, p), alpha) == (p - 1, 0):
+        return None
+    x0 = _f2mul(p, a1, a)
+    if alpha == (p - 1, 0):
+        return _f2mul(p, (0, 1), x0)
+    return _f2mul(p, _f2pow(p, _f2add(p, (1, 0), alpha), (p - 1) // 2), x0)
+
+
+def _twist(p, r, b, trace):
+    import math
+    t2 = trace * trace - 2 * p
+    f = math.isqrt((4 * p * p - t2 * t2) // 3)
+    orders = {p * p + 1 - (s1 * 3 * f + s2 * t2) // 2 for s1 in (1, -1) for s2 in (1, -1)}
+    orders = [n for n in orders if n % r == 0]
+    assert len(orders) == 1
+    return orders[0]
+
+
+def _g2_smul(p, Q, k):
+    def add(P, Q):
+        if P is None:
+            return Q
+        if Q is None:
+            return P
+        if P[0] == Q[0]:
+            if _f2add(p, P[1], Q[1]) == (0, 0):
+                return None
+            lam = _f2mul(p, _f2mul(p, (3, 0), _f2mul(p, P[0], P[0])), _f2inv(p, _f2mul(p, (2, 0), P[1])))
+        else:
+            lam = _f2mul(p, ((Q[1][0] - P[1][0]) % p, (Q[1][1] - P[1][1]) % p),
+                         _f2inv(p, ((Q[0][0] - P[0][0]) % p, (Q[0][1] - P[0][1]) % p)))
+        l2 = _f2mul(p, lam, lam)
+        x3 = ((l2[0] - P[0][0] - Q[0][0]) % p, (l2[1] - P[0][1] - Q[0][1]) % p)
+        t = _f2mul(p, lam, ((P[0][0] - x3[0]) % p, (P[0][1] - x3[1]) % p))
+        return (x3, ((t[0] - P[1][0]) % p, (t[1] - P[1][1]) % p))
+
+    R = None
+    for bit in bin(k)[2:]:
+        R = add(R, R)
+        if bit == "1":
+            R = add(R, Q)
+    return R
+
+
+BLS_G2 = ((0x024AA2B2F08F0A91260805272DC51051C6E47AD4FA403B02B4510B647AE3D1770BAC0326A805BBEFD48056C8C121BDB8,
+           0x13E02B6052719F607DACD3A088274F65596BD0D09920B61AB5DA61BBDC7F5049334CF11213945D57E5AC7D055D042B7E),
+          (0x0CE5D527727D6E118CC9CDC6DA2E351AADFD9BAA8CBDD3A76D429A695160D12C923AC9CC3BACA289E193548608B82801,
+           0x0606C4A02EA734CC32ACD2B02BC28B99CB3E287E85A763AF267492AB572E99AB3F370D275CEC1DA1AAA9075FF05F79BE))
+
+
+def g2_data(name):
+    """twist, G2 generator, Frobenius constants, loop and hard-part digits"""
+    if name == "BN254":
+        p, r, b, trace = BN_P, BN_R, 2, 6 * U * U + 1
+    else:
+        p, r, b, trace = BLS_P, BLS_R, 4, X + 1
+    order = _twist(p, r, b, trace)
+    xi = (1, 1)
+    d_type = name == "BN254"
+    b2 = _f2mul(p, (b, 0), _f2inv(p, xi)) if d_type else _f2mul(p, (b, 0), xi)
+    if name == "BLS12381":
+        gen = BLS_G2
+    else:  # deterministic: first x = k + i on the twist, smaller root, cofactor cleared
+        k = 1
+        while True:
+            x = (k, 1)
+            y = _f2sqrt(p, _f2add(p, _f2mul(p, _f2mul(p, x, x), x), b2))
+            if y is not None:
+                ny = ((-y[0]) % p, (-y[1]) % p)
+                if (ny[1], ny[0]) < (y[1], y[0]):
+                    y = ny
+                gen = _g2_smul(p, (x, y), order // r)
+                if gen is not None:
+                    break
+            k += 1
+    assert _g2_smul(p, gen, r) is None
+    frob = [_f2pow(p, xi, kk * (p - 1) // 6) for kk in range(6)]
+    twx = _f2pow(p, xi, (p - 1) // 3)
+    twy = _f2pow(p, xi, (p - 1) // 2)
+    loop = 6 * U + 2 if name == "BN254" else X
+    hard = (p ** 4 - p ** 2 + 1) // r
+    digits = []
+    for _ in range(4):
+        digits.append(hard % p)
+        hard //= p
+    assert hard == 0
+    return dict(p=p, b2=b2, gen=gen, frob=frob, twx=twx, twy=twy, loop=loop, digits=digits, d_type=d_type)
+
+
+def pairing_struct(name, L, nw):
+    d = g2_data(name)
+    p = d["p"]
+
+    def m29(v):
+        return arr29(mont29(v, p, L), L)
+
+    def f2(a):
+        return "{%s, %s}" % (m29(a[0]), m29(a[1]))
+
+    lines = [
+        "struct %sPair {" % name,
+        "  static constexpr bool D_TWIST = %s;  // D: y^2 = x^3 + b/xi, M: y^2 = x^3 + b xi" % (
+            "true" if d["d_type"] else "false"),
+        "  static constexpr uint32_t B2[2][%d] = %s;  // twist b' (radix-2^29 Montgomery)" % (L, f2(d["b2"])),
+        "  static constexpr uint32_t G2X[2][%d] = %s;" % (L, f2(d["gen"][0])),
+        "  static constexpr uint32_t G2Y[2][%d] = %s;" % (L, f2(d["gen"][1])),
+        "  // Fp12 Frobenius: coefficient of w^k picks up xi^(k (p-1)/6)",
+        "  static constexpr uint32_t FROB[6][2][%d] = {%s};" % (L, ", ".join(f2(g) for g in d["frob"])),
+        "  // twist Frobenius (D-type): x -> conj(x) xi^((p-1)/3), y -> conj(y) xi^((p-1)/2)",
+        "  static constexpr uint32_t TWX[2][%d] = %s;" % (L, f2(d["twx"])),
+        "  static constexpr uint32_t TWY[2][%d] = %s;" % (L, f2(d["twy"])),
+        "  // Miller loop count |%s| (LOOP_BITS bits, two 64-bit words)" % ("6u+2" if name == "BN254" else "x"),
+        "  static constexpr uint64_t LOOP[2] = {0x%016xull, 0x%016xull};" % (abs(d["loop"]) & (2**64 - 1), abs(d["loop"]) >> 64),
+        "  static constexpr int LOOP_BITS = %d;" % abs(d["loop"]).bit_length(),
+        "  static constexpr bool LOOP_NEG = %s;" % ("true" if d["loop"] < 0 else "false"),
+        "  static constexpr int NW = %d;" % nw,
+        "  // (p^4 - p^2 + 1)/r = sum_i HARD[i] p^i (canonical words)",
+        "  static constexpr uint32_t HARD[4][%d] = {%s};" % (nw, ", ".join(arr(v, nw) for v in d["digits"])),
+        "  static constexpr int HARD_BITS = %d;" % max(v.bit_length() for v in d["digits"]),
+        "};",
+    ]
+    return "\n".join(lines)
+
+
 def main():
     out = [
         "// GENERATED by gen_consts.py -- do not edit.",
@@ -125,6 +282,8 @@ def main():
         "  static constexpr uint32_t GX29[14] = %s;" % arr29(mont29(BLS_GX, BLS_P, 14), 14),
         "  static constexpr uint32_t GY29[14] = %s;" % arr29(mont29(BLS_GY, BLS_P, 14), 14),
         "};",
+        pairing_struct("BN254", 9, 8),
+        pairing_struct("BLS12381", 14, 12),
         "}  // namespace kzgx",
         "",
     ]

@@ -18,6 +18,9 @@ struct kzgx_ctx {
   kzgx::Ctx c;
   uint32_t* d_srs_canon = nullptr;  // installed SRS, canonical affine
   size_t srs_canon_b = 0;
+  uint32_t* d_srs2_canon = nullptr;  // installed G2 SRS, canonical affine (x.re, x.im, y.re, y.im)
+  size_t srs2_canon_b = 0;
+  size_t n_srs2 = 0;
 };
 
 namespace kzgx {
@@ -130,7 +133,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
-                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon};
+                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   kzgx::fixed_free(&c);
@@ -505,6 +508,156 @@ int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t cou
   KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, ctx->c.stream));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
   *out_is_inf = (int)oi;
+  return KZGX_OK;
+}
+
+/* ---- verify half: G2 SRS, polyeval_G2, pairing, verify_proof ---------------- */
+size_t kzgx_srs_g2_size(const kzgx_ctx* ctx) { return ctx ? ctx->n_srs2 : 0; }
+
+int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!tau || n == 0 || n > 0x7fffffffu) return KZGX_ERR_ARG;
+  const size_t bytes = n * 2 * point_words(ctx) * 4;
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
+  void* d_tau;
+  KZGX_TRY(stage(ctx, 0, 32, &d_tau));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_tau, tau, 32, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::gen_srs_g2_points(&ctx->c, (const uint32_t*)d_tau, start, n, ctx->d_srs2_canon, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  ctx->n_srs2 = n;
+  return KZGX_OK;
+}
+
+int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!xy || n == 0) return KZGX_ERR_ARG;
+  const size_t bytes = n * 2 * point_words(ctx) * 4;
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
+  KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_srs2_canon, xy, bytes, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  ctx->n_srs2 = n;
+  return KZGX_OK;
+}
+
+int kzgx_get_srs_g2(kzgx_ctx* ctx, uint64_t* xy, size_t n) {
+  KZGX_TRY(activate(ctx));
+  if (!xy) return KZGX_ERR_ARG;
+  if (ctx->n_srs2 == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->n_srs2) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(
+      hipMemcpyAsync(xy, ctx->d_srs2_canon, n * 2 * point_words(ctx) * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_g2_validate(kzgx_ctx* ctx, const uint64_t* xy, size_t count, int* ok) {
+  KZGX_TRY(activate(ctx));
+  if (count == 0) return KZGX_OK;
+  if (!xy || !ok) return KZGX_ERR_ARG;
+  const size_t pb = 2 * point_words(ctx) * 4;
+  void *d_p, *d_ok;
+  KZGX_TRY(stage(ctx, 0, count * pb, &d_p));
+  KZGX_TRY(stage(ctx, 1, count * 4, &d_ok));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_p, xy, count * pb, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::g2_validate(&ctx->c, (const uint32_t*)d_p, count, (uint32_t*)d_ok, ctx->c.stream));
+  std::vector<uint32_t> v(count);
+  KZGX_TRY_HIP(hipMemcpyAsync(v.data(), d_ok, count * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  for (size_t k = 0; k < count; k++) ok[k] = (int)v[k];
+  return KZGX_OK;
+}
+
+int kzgx_msm_g2(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out_xy, int* out_is_inf) {
+  KZGX_TRY(activate(ctx));
+  if (!out_xy || !out_is_inf || (n > 0 && !scalars) || n > (1u << 24)) return KZGX_ERR_ARG;
+  if (ctx->n_srs2 == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->n_srs2) return KZGX_ERR_DEGREE;
+  const size_t pb = 2 * point_words(ctx) * 4;
+  void *d_s = nullptr, *d_o;
+  if (n) KZGX_TRY(stage(ctx, 0, n * 32, &d_s));
+  KZGX_TRY(stage(ctx, 1, pb + 16, &d_o));
+  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
+  uint32_t* d_oi = (uint32_t*)((char*)d_o + pb);
+  KZGX_TRY(kzgx::msm_g2(&ctx->c, (const uint32_t*)d_s, ctx->d_srs2_canon, n, (uint32_t*)d_o, d_oi, ctx->c.stream));
+  uint32_t oi = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, pb, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  *out_is_inf = (int)oi;
+  return KZGX_OK;
+}
+
+int kzgx_pairing(kzgx_ctx* ctx, const uint64_t* g1_xy, const int* g1_inf, const uint64_t* g2_xy, const int* g2_inf,
+                 size_t count, uint64_t* out) {
+  KZGX_TRY(activate(ctx));
+  if (count == 0) return KZGX_OK;
+  if (!g1_xy || !g2_xy || !out || count > (1u << 20)) return KZGX_ERR_ARG;
+  const size_t p1 = point_words(ctx) * 4, p2 = 2 * p1, fb = 6 * p1;
+  void *d_1, *d_2, *d_f, *d_o;
+  KZGX_TRY(stage(ctx, 0, count * p1, &d_1));
+  KZGX_TRY(stage(ctx, 1, count * p2, &d_2));
+  KZGX_TRY(stage(ctx, 2, count * 8, &d_f));
+  KZGX_TRY(stage(ctx, 3, count * fb, &d_o));
+  std::vector<uint32_t> f(2 * count);
+  for (size_t k = 0; k < count; k++) {
+    f[k] = g1_inf ? (uint32_t)(g1_inf[k] != 0) : 0u;
+    f[count + k] = g2_inf ? (uint32_t)(g2_inf[k] != 0) : 0u;
+  }
+  KZGX_TRY_HIP(hipMemcpyAsync(d_1, g1_xy, count * p1, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_2, g2_xy, count * p2, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_f, f.data(), count * 8, hipMemcpyHostToDevice, ctx->c.stream));
+  KZGX_TRY(kzgx::pairing_batch(&ctx->c, (const uint32_t*)d_1, (const uint32_t*)d_f, (const uint32_t*)d_2,
+                               (const uint32_t*)d_f + count, count, (uint32_t*)d_o, ctx->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(out, d_o, count * fb, hipMemcpyDeviceToHost, ctx->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return KZGX_OK;
+}
+
+int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, const uint64_t* proof_xy,
+                      int proof_inf, const uint64_t* xs, const uint64_t* ys, size_t npoints, int* ok) {
+  KZGX_TRY(activate(ctx));
+  if (!commit_xy || !proof_xy || !ok || (npoints > 0 && (!xs || !ys)) || npoints > (1u << 24)) return KZGX_ERR_ARG;
+  if (npoints < 1) return KZGX_ERR_ARG;  // "expected_data size must be 1 or greater"
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  *ok = 0;
+  if (npoints >= ctx->c.n_srs) return KZGX_OK;  // trusted_setup.cpp:235-236
+  if (ctx->n_srs2 < npoints + 1) return KZGX_ERR_NO_SRS;
+  hipStream_t st = ctx->c.stream;
+  const size_t n = npoints;
+  const size_t p1 = point_words(ctx) * 4, p2 = 2 * p1, fb = 6 * p1;
+  // one device block: x | y | I | Z | G1 in (commit, proof) | G1 work | G2 in | flags | Fp12 out
+  const size_t o_x = 0, o_y = o_x + n * 32, o_I = o_y + n * 32, o_Z = o_I + n * 32, o_g1 = o_Z + (n + 1) * 32;
+  const size_t o_w = o_g1 + 4 * p1, o_g2 = o_w + 2 * p1, o_f = o_g2 + 2 * p2, o_o = o_f + 64;
+  void* d;
+  KZGX_TRY(stage(ctx, 3, o_o + 2 * fb, &d));
+  char* b = (char*)d;
+  uint32_t* g1 = (uint32_t*)(b + o_g1);  // [proof, p2, commit, msm(I)]
+  uint32_t* fl = (uint32_t*)(b + o_f);   // [proof_inf, p2_inf, p1_inf, srs2_0_inf, commit_inf, msmI_inf]
+  uint32_t hf[8] = {(uint32_t)(proof_inf != 0), 0, 0, 0, (uint32_t)(commit_inf != 0), 0, 0, 0};
+  KZGX_TRY_HIP(hipMemcpyAsync(b + o_x, xs, n * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(b + o_y, ys, n * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(g1, proof_xy, p1, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync((char*)g1 + 2 * p1, commit_xy, p1, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(fl, hf, sizeof(hf), hipMemcpyHostToDevice, st));
+  // I and Z (linear_roots_and_polyfit, util.cpp:172-178)
+  KZGX_TRY(kzgx::poly_interpolate(&ctx->c, (const uint32_t*)(b + o_x), (const uint32_t*)(b + o_y), n,
+                                  (uint32_t*)(b + o_I), st));
+  KZGX_TRY(kzgx::poly_vanishing(&ctx->c, (const uint32_t*)(b + o_x), n, (uint32_t*)(b + o_Z), st));
+  // p2 = C - [I(tau)]G1
+  KZGX_TRY(kzgx::msm_batch(&ctx->c, (const uint32_t*)(b + o_I), n, 1, n * 8, (uint32_t*)((char*)g1 + 3 * p1), fl + 5,
+                           st));
+  KZGX_TRY(kzgx::g1_sub(&ctx->c, (const uint32_t*)((char*)g1 + 2 * p1), fl + 4, (const uint32_t*)((char*)g1 + 3 * p1),
+                        fl + 5, (uint32_t*)((char*)g1 + p1), fl + 1, st));
+  // p1 = [Z(tau)]G2, second pairing's G2 input = G2[0]
+  uint32_t* g2 = (uint32_t*)(b + o_g2);
+  KZGX_TRY(kzgx::msm_g2(&ctx->c, (const uint32_t*)(b + o_Z), ctx->d_srs2_canon, n + 1, g2, fl + 2, st));
+  KZGX_TRY_HIP(hipMemcpyAsync((char*)g2 + p2, ctx->d_srs2_canon, p2, hipMemcpyDeviceToDevice, st));
+  // v1 = e(proof, p1), v2 = e(p2, G2[0])
+  KZGX_TRY(kzgx::pairing_batch(&ctx->c, g1, fl, g2, fl + 2, 2, (uint32_t*)(b + o_o), st));
+  std::vector<uint8_t> v(2 * fb);
+  KZGX_TRY_HIP(hipMemcpyAsync(v.data(), b + o_o, 2 * fb, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  *ok = std::memcmp(v.data(), v.data() + fb, fb) == 0 ? 1 : 0;  // FP12_equals on canonical values
   return KZGX_OK;
 }
 

@@ -100,6 +100,8 @@ struct Ctx {
   size_t poly_ws_b = 0;
   void* d_poly_ws2 = nullptr;  // scratch of the multi-point opening pipeline
   size_t poly_ws2_b = 0;
+  void* d_g2_ws = nullptr;  // G2 MSM terms (pairing.hip)
+  size_t g2_ws_b = 0;
   // staging for host-pointer entry points
   void* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_b[4] = {0, 0, 0, 0};
@@ -156,5 +158,15 @@ int prove_range_poly(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_
                      size_t* nq, hipStream_t st);
 int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
                      hipStream_t st);
+
+// verify path: G2 SRS, polyeval_G2, pairing (pairing.hip)
+int gen_srs_g2_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, uint32_t* d_out, hipStream_t st);
+int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
+           uint32_t* d_out_inf, hipStream_t st);
+int g2_validate(Ctx* ctx, const uint32_t* d_xy, size_t count, uint32_t* d_ok, hipStream_t st);
+int pairing_batch(Ctx* ctx, const uint32_t* d_g1, const uint32_t* d_g1_inf, const uint32_t* d_g2,
+                  const uint32_t* d_g2_inf, size_t count, uint32_t* d_out, hipStream_t st);
+int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
+           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 
 }  // namespace kzgx

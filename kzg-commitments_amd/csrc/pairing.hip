@@ -1,0 +1,344 @@
+// Verify path on gfx950: the G2 half of the setup, polyeval_G2 and the
+// optimal ate pairing behind trusted_setup::verify_proof
+// (reference src/trusted_setup.cpp:123-135 G2 SRS, :176-201 polyeval_G2,
+// :230-254 verify_proof with miracl PAIR_ate + PAIR_fexp).
+//
+// Pairing: Miller loop on the twist in Jacobian coordinates with the line
+// functions evaluated at P and placed as sparse Fp12 elements, then the
+// exact final exponentiation f^((p^12 - 1)/r):
+//   easy part   f^(p^6 - 1)(p^2 + 1)       (conjugate, inverse, Frobenius)
+//   hard part   f^((p^4 - p^2 + 1)/r), written in base p as
+//               sum_i HARD[i] p^i, so f^hard = prod_i frob^i(f)^HARD[i],
+//               one joint square-and-multiply over a 16-entry table.
+// BN254 (miracl Nogami, u < 0, D-type twist): loop |6u + 2|, then
+// conjugate (u < 0), then the two Frobenius lines l_{T, pi(Q)},
+// l_{T + pi(Q), -pi^2(Q)}.  BLS12-381 (x < 0, M-type twist): loop |x|, then
+// conjugate.  Line functions are computed up to factors in proper subfields
+// (Fp2, Fp4), which the final exponentiation removes, so the value is the
+// unique pairing value -- bit-exact with the oracle's definitional pairing
+// (oracle/pairing_ref.py).
+//
+// One pairing per thread: a verify needs two, so this is latency-bound
+// single-lane code by design; many pairings (batched verifies) fill waves.
+#include <hip/hip_runtime.h>
+
+#include "kzgx_internal.hpp"
+#include "tower.hpp"
+
+namespace kzgx {
+
+// ---- Miller loop ----------------------------------------------------------------
+// place the scaled line  w0 + w1 w + w3 w^3 (D-type) or
+// (w0 + w1 w^-1 + w3 w^-3) w^3 (M-type) into Fp12
+template <class C>
+KZGX_DEV Fp12<C> line_to_f12(const Fp2<C>& w0, const Fp2<C>& w1, const Fp2<C>& w3) {
+  using P = typename PairOf<C>::T;
+  Fp12<C> l;
+  l.c0 = f6_zero<C>();
+  l.c1 = f6_zero<C>();
+  if (P::D_TWIST) {
+    l.c0.c0 = w0;  // w^0
+    l.c1.c0 = w1;  // w^1
+    l.c1.c1 = w3;  // w^3 = w v
+  } else {
+    l.c0.c0 = w3;  // w^0
+    l.c0.c1 = w1;  // w^2 = v
+    l.c1.c1 = w0;  // w^3
+  }
+  return l;
+}
+
+// tangent at T evaluated at P = (xp, yp), scaled by 2 Y Z^3; T <- 2T
+template <class C>
+KZGX_TW Fp12<C> line_dbl(G2J<C>& T, const F29<typename C::Fp29>& xp, const F29<typename C::Fp29>& yp) {
+  const Fp2<C> A = f2_sqr<C>(T.X);
+  const Fp2<C> B = f2_sqr<C>(T.Y);
+  const Fp2<C> E = f2_add<C>(f2_dbl<C>(A), A);
+  const Fp2<C> ZZ = f2_sqr<C>(T.Z);
+  const Fp2<C> Z3 = f2_dbl<C>(f2_mul<C>(T.Y, T.Z));
+  const Fp2<C> w0 = f2_mul_fp<C>(f2_mul<C>(Z3, ZZ), yp);
+  const Fp2<C> w1 = f2_neg<C>(f2_mul_fp<C>(f2_mul<C>(E, ZZ), xp));
+  const Fp2<C> w3 = f2_sub<C>(f2_mul<C>(E, T.X), f2_dbl<C>(B));
+  T = g2_dbl<C>(T);
+  return line_to_f12<C>(w0, w1, w3);
+}
+
+// line through T and q (affine) evaluated at P, scaled by 2 Z H; T <- T + q
+template <class C>
+KZGX_TW Fp12<C> line_add(G2J<C>& T, const G2A<C>& q, const F29<typename C::Fp29>& xp,
+                         const F29<typename C::Fp29>& yp) {
+  const Fp2<C> Z1Z1 = f2_sqr<C>(T.Z);
+  const Fp2<C> U2 = f2_mul<C>(q.x, Z1Z1);
+  const Fp2<C> S2 = f2_mul<C>(q.y, f2_mul<C>(T.Z, Z1Z1));
+  const Fp2<C> H = f2_sub<C>(U2, T.X);
+  const Fp2<C> rr = f2_dbl<C>(f2_sub<C>(S2, T.Y));
+  const Fp2<C> Z3 = f2_dbl<C>(f2_mul<C>(T.Z, H));
+  const Fp2<C> w0 = f2_mul_fp<C>(Z3, yp);
+  const Fp2<C> w1 = f2_neg<C>(f2_mul_fp<C>(rr, xp));
+  const Fp2<C> w3 = f2_sub<C>(f2_mul<C>(rr, q.x), f2_mul<C>(q.y, Z3));
+  T = g2_add_mixed<C>(T, q);
+  return line_to_f12<C>(w0, w1, w3);
+}
+
+// pi(q) on the D-type twist: (conj(x) xi^((p-1)/3), conj(y) xi^((p-1)/2))
+template <class C>
+KZGX_DEV G2A<C> twist_frob(const G2A<C>& q) {
+  using P = typename PairOf<C>::T;
+  G2A<C> r;
+  r.x = f2_mul<C>(f2_conj<C>(q.x), f2_const<C>(P::TWX));
+  r.y = f2_mul<C>(f2_conj<C>(q.y), f2_const<C>(P::TWY));
+  return r;
+}
+
+template <class C>
+KZGX_TW Fp12<C> miller_loop(const Affine<C>& p, const G2A<C>& q) {
+  using P = typename PairOf<C>::T;
+  Fp12<C> f = f12_one<C>();
+  G2J<C> T = g2_from_affine<C>(q);
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    f = f12_sqr<C>(f);
+    f = f12_mul<C>(f, line_dbl<C>(T, p.x, p.y));
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) f = f12_mul<C>(f, line_add<C>(T, q, p.x, p.y));
+  }
+  if (P::LOOP_NEG) {  // f_{-n} = 1/f_n up to a vertical line; 1/f == conj(f) after the final exponentiation
+    f = f12_conj<C>(f);
+    T.Y = f2_neg<C>(T.Y);
+  }
+  if (P::D_TWIST) {  // BN optimal ate: the two Frobenius lines
+    const G2A<C> q1 = twist_frob<C>(q);
+    G2A<C> q2 = twist_frob<C>(q1);
+    q2.y = f2_neg<C>(q2.y);
+    f = f12_mul<C>(f, line_add<C>(T, q1, p.x, p.y));
+    f = f12_mul<C>(f, line_add<C>(T, q2, p.x, p.y));
+  }
+  return f;
+}
+
+template <class C>
+KZGX_TW Fp12<C> final_exp(const Fp12<C>& f) {
+  using P = typename PairOf<C>::T;
+  // easy part: f^(p^6 - 1) (p^2 + 1)
+  Fp12<C> g = f12_mul<C>(f12_conj<C>(f), f12_inv<C>(f));
+  g = f12_mul<C>(f12_frob<C>(f12_frob<C>(g)), g);
+  // hard part: prod_i frob^i(g)^HARD[i]
+  Fp12<C> tab[16];
+  Fp12<C> b[4];
+  b[0] = g;
+  for (int i = 1; i < 4; i++) b[i] = f12_frob<C>(b[i - 1]);
+  tab[0] = f12_one<C>();
+  for (int m = 1; m < 16; m++) {
+    const int low = __builtin_ctz(m);
+    const int rest = m & (m - 1);
+    tab[m] = rest ? f12_mul<C>(tab[rest], b[low]) : b[low];
+  }
+  Fp12<C> acc = f12_one<C>();
+  for (int bit = P::HARD_BITS - 1; bit >= 0; bit--) {
+    acc = f12_sqr<C>(acc);
+    int idx = 0;
+    for (int i = 0; i < 4; i++) idx |= (int)((P::HARD[i][bit >> 5] >> (bit & 31)) & 1u) << i;
+    if (idx) acc = f12_mul<C>(acc, tab[idx]);
+  }
+  return acc;
+}
+
+// thread per pairing: e(P_k, Q_k) for canonical affine inputs (all-zero or
+// flagged = infinity -> 1), canonical Fp12 out in tower order
+template <class C>
+__global__ __launch_bounds__(64) void k_pairing(const uint32_t* __restrict__ g1, const uint32_t* __restrict__ g1_inf,
+                                                const uint32_t* __restrict__ g2, const uint32_t* __restrict__ g2_inf,
+                                                uint32_t count, uint32_t* __restrict__ out) {
+  constexpr int N = C::Fp::N;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  Affine<C> p;
+  G2A<C> q;
+  const bool pf = affine_from_canonical<C>(g1 + (size_t)k * 2 * N, p) && !(g1_inf && g1_inf[k]);
+  const bool qf = g2_from_canon<C>(g2 + (size_t)k * 4 * N, q) && !(g2_inf && g2_inf[k]);
+  Fp12<C> r = f12_one<C>();
+  if (pf && qf) r = final_exp<C>(miller_loop<C>(p, q));
+  f12_to_canon<C>(r, out + (size_t)k * 12 * N);
+}
+
+// ---- G2 SRS and polyeval_G2 ---------------------------------------------------------
+// [tau^(start + i)] G2, thread per point (generate_elements_range,
+// trusted_setup.cpp:123-135)
+template <class C>
+KZGX_TW G2J<C> g2_mul_words(const G2A<C>& q, const uint32_t (&e)[8]) {
+  G2J<C> acc = g2_inf<C>();
+  for (int b = 255; b >= 0; b--) {
+    acc = g2_dbl<C>(acc);
+    if ((e[b >> 5] >> (b & 31)) & 1u) acc = g2_add_mixed<C>(acc, q);
+  }
+  return acc;
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void k_gen_srs_g2(const uint32_t* __restrict__ tau_canon, uint64_t start,
+                                                   uint32_t n, uint32_t* __restrict__ out) {
+  using P = typename PairOf<C>::T;
+  using FR = typename C::Fr;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fe<FR> tm = fe_to_mont<FR>(fe_load<FR>(tau_canon));
+  const uint64_t ex = start + i;
+  Fe<FR> e = fe_one<FR>();
+  for (int b = 63; b >= 0; b--) {
+    e = fe_sqr<FR>(e);
+    if ((ex >> b) & 1ull) e = fe_mul<FR>(e, tm);
+  }
+  e = fe_from_mont<FR>(e);
+  G2A<C> g;
+  g.x = f2_const<C>(P::G2X);
+  g.y = f2_const<C>(P::G2Y);
+  uint32_t ew[8];
+  for (int k = 0; k < 8; k++) ew[k] = e.v[k];
+  G2A<C> a;
+  const bool fin = g2_to_affine<C>(g2_mul_words<C>(g, ew), a);
+  g2_to_canon<C>(a, fin, out + (size_t)i * 4 * C::Fp::N);
+}
+
+// term i: c_i [tau^i]G2 (canonical scalar words, SRS canonical affine), Jacobian out
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_terms(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ srs2,
+                                                 uint32_t n, G2J<C>* __restrict__ terms) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2A<C> q;
+  const bool fin = g2_from_canon<C>(srs2 + (size_t)i * 4 * C::Fp::N, q);
+  uint32_t e[8];
+  for (int k = 0; k < 8; k++) e[k] = scalars[(size_t)i * 8 + k];
+  terms[i] = fin ? g2_mul_words<C>(q, e) : g2_inf<C>();
+}
+
+// one workgroup of 64: strided partial sums, then lane 0 folds and normalizes
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_sum(const G2J<C>* __restrict__ terms, uint32_t n, G2J<C>* __restrict__ part,
+                                               uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  const uint32_t t = threadIdx.x;
+  G2J<C> acc = g2_inf<C>();
+  for (uint32_t i = t; i < n; i += 64) acc = g2_add<C>(acc, terms[i]);
+  part[t] = acc;
+  __syncthreads();
+  if (t != 0) return;
+  for (uint32_t k = 1; k < 64; k++) acc = g2_add<C>(acc, part[k]);
+  G2A<C> a;
+  const bool fin = g2_to_affine<C>(acc, a);
+  g2_to_canon<C>(a, fin, out);
+  *out_inf = fin ? 0u : 1u;
+}
+
+// ok[k] = 1 if point k is a valid (finite) G2 point: coordinates < m and on
+// the twist y^2 = x^3 + b'
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_validate(const uint32_t* __restrict__ xy, uint32_t count,
+                                                    uint32_t* __restrict__ ok) {
+  using P = typename PairOf<C>::T;
+  constexpr int N = C::Fp::N;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint32_t* w = xy + (size_t)k * 4 * N;
+  bool lt = true;
+  for (int c = 0; c < 4; c++) lt = lt && canon_lt_m<C>(w + c * N);
+  G2A<C> q;
+  const bool fin = g2_from_canon<C>(w, q);
+  const Fp2<C> d = f2_sub<C>(f2_sqr<C>(q.y), f2_add<C>(f2_mul<C>(f2_sqr<C>(q.x), q.x), f2_const<C>(P::B2)));
+  ok[k] = (lt && fin && f2_is_zero<C>(d)) ? 1u : 0u;
+}
+
+// out = a - b for canonical affine G1 points (the C - [I(tau)]G1 of
+// verify_proof, trusted_setup.cpp:245-247)
+template <class C>
+__global__ void k_g1_sub(const uint32_t* __restrict__ a, const uint32_t* __restrict__ a_inf,
+                         const uint32_t* __restrict__ b, const uint32_t* __restrict__ b_inf, uint32_t* __restrict__ out,
+                         uint32_t* __restrict__ out_inf) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Xyzz<C> acc = xyzz_inf<C>();
+  Affine<C> pa, pb;
+  if (affine_from_canonical<C>(a, pa) && !(a_inf && *a_inf)) acc = xyzz_from_affine<C>(pa);
+  if (affine_from_canonical<C>(b, pb) && !(b_inf && *b_inf)) acc = xyzz_add_affine<C>(acc, affine_neg<C>(pb));
+  Affine<C> r;
+  const bool fin = xyzz_to_affine<C>(acc, r);
+  affine_to_canonical<C>(out, r, fin);
+  *out_inf = fin ? 0u : 1u;
+}
+
+// ---- host side ----------------------------------------------------------------
+template <class C>
+static int pairing_impl(const uint32_t* g1, const uint32_t* g1_inf, const uint32_t* g2, const uint32_t* g2_inf,
+                        size_t count, uint32_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pairing<C>, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, st, g1, g1_inf, g2, g2_inf,
+                     (uint32_t)count, out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int pairing_batch(Ctx* ctx, const uint32_t* d_g1, const uint32_t* d_g1_inf, const uint32_t* d_g2,
+                  const uint32_t* d_g2_inf, size_t count, uint32_t* d_out, hipStream_t st) {
+  if (count == 0) return KZGX_OK;
+  return ctx->curve == KZGX_CURVE_BN254 ? pairing_impl<BN254G1>(d_g1, d_g1_inf, d_g2, d_g2_inf, count, d_out, st)
+                                        : pairing_impl<BLS12381G1>(d_g1, d_g1_inf, d_g2, d_g2_inf, count, d_out, st);
+}
+
+int gen_srs_g2_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, uint32_t* d_out, hipStream_t st) {
+  dim3 blk(64), grd((unsigned)((n + 63) / 64));
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_gen_srs_g2<BN254G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, d_out);
+  else
+    hipLaunchKernelGGL(k_gen_srs_g2<BLS12381G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, d_out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+template <class C>
+static int msm_g2_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
+                       uint32_t* d_out_inf, hipStream_t st) {
+  const size_t tb = (n + 64) * sizeof(G2J<C>);
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_g2_ws, tb, &ctx->g2_ws_b));
+  G2J<C>* terms = (G2J<C>*)ctx->d_g2_ws;
+  G2J<C>* part = terms + n;
+  {
+    ProfScope p(ctx, st, "g2_terms");
+    hipLaunchKernelGGL(k_g2_terms<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_scalars, d_srs2,
+                       (uint32_t)n, terms);
+  }
+  hipLaunchKernelGGL(k_g2_sum<C>, dim3(1), dim3(64), 0, st, terms, (uint32_t)n, part, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
+           uint32_t* d_out_inf, hipStream_t st) {
+  if (n == 0) {  // ECP2_inf (trusted_setup.cpp:177-181)
+    const size_t pb = 4 * (size_t)ctx->base_words() * 4;
+    KZGX_TRY_HIP(hipMemsetAsync(d_out, 0, pb, st));
+    const uint32_t one = 1;
+    KZGX_TRY_HIP(hipMemcpyAsync(d_out_inf, &one, 4, hipMemcpyHostToDevice, st));
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+    return KZGX_OK;
+  }
+  return ctx->curve == KZGX_CURVE_BN254 ? msm_g2_impl<BN254G1>(ctx, d_scalars, d_srs2, n, d_out, d_out_inf, st)
+                                        : msm_g2_impl<BLS12381G1>(ctx, d_scalars, d_srs2, n, d_out, d_out_inf, st);
+}
+
+int g2_validate(Ctx* ctx, const uint32_t* d_xy, size_t count, uint32_t* d_ok, hipStream_t st) {
+  if (count == 0) return KZGX_OK;
+  dim3 blk(64), grd((unsigned)((count + 63) / 64));
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g2_validate<BN254G1>, grd, blk, 0, st, d_xy, (uint32_t)count, d_ok);
+  else
+    hipLaunchKernelGGL(k_g2_validate<BLS12381G1>, grd, blk, 0, st, d_xy, (uint32_t)count, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
+           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g1_sub<BN254G1>, dim3(1), dim3(64), 0, st, d_a, d_a_inf, d_b, d_b_inf, d_out, d_out_inf);
+  else
+    hipLaunchKernelGGL(k_g1_sub<BLS12381G1>, dim3(1), dim3(64), 0, st, d_a, d_a_inf, d_b, d_b_inf, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+}  // namespace kzgx

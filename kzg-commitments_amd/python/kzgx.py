@@ -26,6 +26,8 @@ EXPORTS = [
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
+    "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
+    "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof",
 ]
 
 _lib = None
@@ -79,6 +81,14 @@ def lib():
             "kzgx_poly_vanishing": (ctypes.c_int, [vp, u64p, sz, u64p]),
             "kzgx_g1_validate": (ctypes.c_int, [vp, u64p, intp]),
             "kzgx_g1_sum": (ctypes.c_int, [vp, u64p, intp, sz, u64p, intp]),
+            "kzgx_gen_srs_g2": (ctypes.c_int, [vp, u64p, sz, sz]),
+            "kzgx_load_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
+            "kzgx_get_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
+            "kzgx_srs_g2_size": (sz, [vp]),
+            "kzgx_g2_validate": (ctypes.c_int, [vp, u64p, sz, intp]),
+            "kzgx_msm_g2": (ctypes.c_int, [vp, u64p, sz, u64p, intp]),
+            "kzgx_pairing": (ctypes.c_int, [vp, u64p, intp, u64p, intp, sz, u64p]),
+            "kzgx_verify_proof": (ctypes.c_int, [vp, u64p, ctypes.c_int, u64p, ctypes.c_int, u64p, u64p, sz, intp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -272,3 +282,60 @@ class Context:
         _chk(lib().kzgx_g1_sum(self.h, _p(pts), None if f is None else f.ctypes.data_as(intp), pts.shape[0],
                                _p(out), ctypes.byref(oi)), "kzgx_g1_sum")
         return out, bool(oi.value)
+
+    # ---- verify half: G2 setup, polyeval_G2, pairing ----
+    # G2 points: (n, 4 * W64) uint64 = x.re || x.im || y.re || y.im; Fp12: (12 * W64,)
+    @property
+    def srs2_size(self) -> int:
+        return lib().kzgx_srs_g2_size(self.h)
+
+    def gen_srs_g2(self, tau: int, n: int, start: int = 0):
+        t = np.array([(tau >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+        _chk(lib().kzgx_gen_srs_g2(self.h, _p(t), start, n), "kzgx_gen_srs_g2")
+
+    def load_srs_g2(self, xy: np.ndarray):
+        xy = np.ascontiguousarray(xy, dtype=np.uint64).reshape(-1, 4 * self.w64)
+        _chk(lib().kzgx_load_srs_g2(self.h, _p(xy), xy.shape[0]), "kzgx_load_srs_g2")
+
+    def get_srs_g2(self, n: int | None = None) -> np.ndarray:
+        n = self.srs2_size if n is None else n
+        out = np.zeros((n, 4 * self.w64), dtype=np.uint64)
+        _chk(lib().kzgx_get_srs_g2(self.h, _p(out), n), "kzgx_get_srs_g2")
+        return out
+
+    def g2_validate(self, xy: np.ndarray) -> np.ndarray:
+        xy = np.ascontiguousarray(xy, dtype=np.uint64).reshape(-1, 4 * self.w64)
+        ok = np.zeros(xy.shape[0], dtype=np.int32)
+        _chk(lib().kzgx_g2_validate(self.h, _p(xy), xy.shape[0], ok.ctypes.data_as(intp)), "kzgx_g2_validate")
+        return ok.astype(bool)
+
+    def msm_g2(self, scalars: np.ndarray):
+        sc = as_scalars(scalars) if len(scalars) else np.zeros((0, 4), dtype=np.uint64)
+        out = np.zeros(4 * self.w64, dtype=np.uint64)
+        inf = ctypes.c_int(0)
+        _chk(lib().kzgx_msm_g2(self.h, _p(sc) if sc.shape[0] else None, sc.shape[0], _p(out), ctypes.byref(inf)),
+             "kzgx_msm_g2")
+        return out, bool(inf.value)
+
+    def pairing(self, g1: np.ndarray, g2: np.ndarray, g1_inf=None, g2_inf=None) -> np.ndarray:
+        a = np.ascontiguousarray(g1, dtype=np.uint64).reshape(-1, 2 * self.w64)
+        b = np.ascontiguousarray(g2, dtype=np.uint64).reshape(-1, 4 * self.w64)
+        assert a.shape[0] == b.shape[0]
+        fa = None if g1_inf is None else np.ascontiguousarray(g1_inf, dtype=np.int32)
+        fb = None if g2_inf is None else np.ascontiguousarray(g2_inf, dtype=np.int32)
+        out = np.zeros((a.shape[0], 12 * self.w64), dtype=np.uint64)
+        _chk(lib().kzgx_pairing(self.h, _p(a), None if fa is None else fa.ctypes.data_as(intp), _p(b),
+                                None if fb is None else fb.ctypes.data_as(intp), a.shape[0], _p(out)),
+             "kzgx_pairing")
+        return out
+
+    def verify_proof(self, commit, commit_inf: bool, proof, proof_inf: bool, xs, ys) -> bool:
+        c = np.ascontiguousarray(commit, dtype=np.uint64).reshape(2 * self.w64)
+        p = np.ascontiguousarray(proof, dtype=np.uint64).reshape(2 * self.w64)
+        x = as_scalars(xs) if len(xs) else np.zeros((0, 4), dtype=np.uint64)
+        y = as_scalars(ys) if len(ys) else np.zeros((0, 4), dtype=np.uint64)
+        ok = ctypes.c_int(0)
+        _chk(lib().kzgx_verify_proof(self.h, _p(c), int(commit_inf), _p(p), int(proof_inf),
+                                     _p(x) if x.shape[0] else None, _p(y) if y.shape[0] else None, x.shape[0],
+                                     ctypes.byref(ok)), "kzgx_verify_proof")
+        return bool(ok.value)
