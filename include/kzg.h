@@ -56,6 +56,17 @@ struct G1 {
   bool operator!=(const G1& o) const { return !(*this == o); }
 };
 
+/** Affine G2 point on the sextic twist (the reference's miracl ECP2):
+ *  x = x0 + x1 i, y = y0 + y1 i, canonical coordinates. */
+struct G2 {
+  std::array<uint64_t, 6> x0{}, x1{}, y0{}, y1{};
+  bool inf = true;
+  bool operator==(const G2& o) const {
+    return inf == o.inf && (inf || (x0 == o.x0 && x1 == o.x1 && y0 == o.y0 && y1 == o.y1));
+  }
+  bool operator!=(const G2& o) const { return !(*this == o); }
+};
+
 /** Initialize the library (BN254, the reference's default build). */
 void init();
 /** Extension: pick the curve at run time (KZGX_CURVE_BN254 / KZGX_CURVE_BLS12381). */
@@ -123,13 +134,14 @@ class trusted_setup {
   G1 polyeval_G1(const std::vector<Fr>& P);
 
  public:
-  /** random tau (std::random_device), [tau^i]G1 for i < num_coeff, on the GPU
-   *  @throws std::invalid_argument if num_coeff < 2 */
+  /** random tau (std::random_device), [tau^i]G1 and [tau^i]G2 for
+   *  i < num_coeff, on the GPU  @throws std::invalid_argument if num_coeff < 2 */
   trusted_setup(int num_coeff);
   /** Extension: deterministic setup from a given tau (tests, benchmarks). */
   trusted_setup(int num_coeff, const Fr& tau);
-  /** load a setup written by export_setup (G1 part; trusted_setup.cpp:76-101)
-   *  @throws std::runtime_error for an inaccessible / bad file */
+  /** load a setup written by export_setup (trusted_setup.cpp:76-121)
+   *  @throws std::runtime_error for an inaccessible file or a bad G1 record,
+   *          std::logic_error for a bad G2 record (as the reference does) */
   trusted_setup(const std::string& filename);
   ~trusted_setup();
   trusted_setup(const trusted_setup&) = delete;
@@ -146,18 +158,22 @@ class trusted_setup {
   proof create_proof(const kzg::poly& poly, int byte_offset, int byte_length, int chunk_size);
   /** @throws std::invalid_argument if chunk_length < 1 */
   proof create_proof(const kzg::poly& poly, int chunk_offset, int chunk_length);
-  /** pairing check (trusted_setup.cpp:230-254).  Needs the G2 half of the
-   *  setup, which this round does not build yet: throws std::logic_error. */
+  /** e(proof, [Z(s)]2) == e(C - [I(s)]1, [1]2), all on the GPU
+   *  (trusted_setup.cpp:230-254)
+   *  @throws std::invalid_argument if expected_data is empty; false if it
+   *          holds >= size() points */
   bool verify_proof(commit& commit, proof& proof, blob& expected_data);
-  /** writes the reference file layout (u64 n, n x (u32 len, G1 octet), ...);
-   *  the G2 half is not built yet: throws std::logic_error. */
+  /** writes the reference file layout (trusted_setup.cpp:256-287):
+   *  u64 n, n x (u32 len, G1 octet), n x (u32 len, G2 octet); prints
+   *  "failed to export" and returns if the file cannot be opened */
   void export_setup(const std::string& filename = "kzg_public");
 
   /** Extensions: batched commits / single-point openings in one GPU pass. */
   std::vector<commit> create_commits(const std::vector<kzg::poly>& polys);
   std::vector<proof> create_proofs(const kzg::poly& poly, const std::vector<long>& points);
-  /** copy of the G1 SRS points */
+  /** copy of the G1 / G2 SRS points */
   std::vector<G1> g1_points() const;
+  std::vector<G2> g2_points() const;
 };
 
 }  // namespace kzg

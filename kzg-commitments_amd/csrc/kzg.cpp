@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <fstream>
+#include <iostream>
 #include <mutex>
 #include <random>
 
@@ -108,6 +109,50 @@ std::vector<uint8_t> ecp_serialize(const G1& g) {
   std::memcpy(out.data(), &len, 4);
   out.insert(out.end(), oct.begin(), oct.end());
   return out;
+}
+
+// ECP2_toOctet(..., false): 0x04 || x || y, each Fp2 as imag || real,
+// MODBYTES big-endian each (miracl-core's current FP2_toBytes order; recalled,
+// version-dependent).  Infinity: ECP2_inf = (0, 1).
+void put_be(uint8_t* dst, const uint64_t* limbs, size_t mb) {
+  for (size_t k = 0; k < mb; k++) dst[mb - 1 - k] = (uint8_t)(limbs[k / 8] >> (8 * (k % 8)));
+}
+void get_be(const uint8_t* src, uint64_t* limbs, size_t mb) {
+  for (size_t k = 0; k < mb; k++) limbs[k / 8] |= (uint64_t)src[mb - 1 - k] << (8 * (k % 8));
+}
+
+std::vector<uint8_t> ecp2_octet(const G2& g) {
+  const size_t mb = mod_bytes();
+  std::vector<uint8_t> oct(1 + 4 * mb, 0);
+  oct[0] = 0x04;
+  std::array<uint64_t, 6> x0 = g.x0, x1 = g.x1, y0 = g.y0, y1 = g.y1;
+  if (g.inf) {
+    x0.fill(0);
+    x1.fill(0);
+    y0.fill(0);
+    y1.fill(0);
+    y0[0] = 1;
+  }
+  put_be(&oct[1], x1.data(), mb);
+  put_be(&oct[1 + mb], x0.data(), mb);
+  put_be(&oct[1 + 2 * mb], y1.data(), mb);
+  put_be(&oct[1 + 3 * mb], y0.data(), mb);
+  return oct;
+}
+
+// G2 canonical words (x.re, x.im, y.re, y.im; base_limbs() each) <-> G2
+G2 to_g2(const uint64_t* w, bool inf) {
+  G2 g;
+  const int nl = base_limbs();
+  g.inf = inf;
+  if (!inf)
+    for (int i = 0; i < nl; i++) {
+      g.x0[i] = w[i];
+      g.x1[i] = w[nl + i];
+      g.y0[i] = w[2 * nl + i];
+      g.y1[i] = w[3 * nl + i];
+    }
+  return g;
 }
 
 // deserialize_ECP (util.cpp:98-115): anything that is not a valid on-curve
@@ -276,7 +321,9 @@ trusted_setup::trusted_setup(int num_coeff) {
   Fr tau = Fr::from_le_bytes(seed, 32);
   check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
   check(kzgx_gen_srs_g1(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g1");
+  check(kzgx_gen_srs_g2(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g2");
   n = (size_t)num_coeff;
+  tau.v.fill(0);
   std::memset(seed, 0, sizeof seed);  // tau is toxic waste; the reference discards it too
 }
 
@@ -284,6 +331,7 @@ trusted_setup::trusted_setup(int num_coeff, const Fr& tau) {
   if (num_coeff < 2) throw std::invalid_argument("num_coeff must be at least 2");
   check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
   check(kzgx_gen_srs_g1(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g1");
+  check(kzgx_gen_srs_g2(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g2");
   n = (size_t)num_coeff;
 }
 
@@ -314,8 +362,32 @@ trusted_setup::trusted_setup(const std::string& filename) {
       xy[2 * nl * i + nl + k] = g.y[k];
     }
   }
+  // G2 records (trusted_setup.cpp:103-118); a bad one is a logic_error there
+  std::vector<uint64_t> xy2(4 * nl * num, 0);
+  for (uint64_t i = 0; i < num; i++) {
+    uint32_t len = 0;
+    f.read(reinterpret_cast<char*>(&len), 4);
+    if (!f || len != 1 + 4 * mb) throw std::logic_error("bad trusted setup file");
+    std::vector<uint8_t> oct(len);
+    f.read(reinterpret_cast<char*>(oct.data()), len);
+    if (!f || oct[0] != 0x04) throw std::logic_error("bad trusted setup file");
+    uint64_t* w = &xy2[4 * nl * i];
+    get_be(&oct[1], w + nl, mb);           // x.im
+    get_be(&oct[1 + mb], w, mb);           // x.re
+    get_be(&oct[1 + 2 * mb], w + 3 * nl, mb);  // y.im
+    get_be(&oct[1 + 3 * mb], w + 2 * nl, mb);  // y.re
+  }
   check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
+  std::vector<int> ok(num, 0);
+  check(kzgx_g2_validate(ctx, xy2.data(), num, ok.data()), "kzgx_g2_validate");
+  for (uint64_t i = 0; i < num; i++)
+    if (!ok[i]) {
+      kzgx_destroy(ctx);
+      ctx = nullptr;
+      throw std::logic_error("bad trusted setup file");
+    }
   check(kzgx_load_srs_g1(ctx, xy.data(), num), "kzgx_load_srs_g1");
+  check(kzgx_load_srs_g2(ctx, xy2.data(), num), "kzgx_load_srs_g2");
   n = num;
 }
 
@@ -395,14 +467,49 @@ proof trusted_setup::create_proof(const kzg::poly& p, int chunk_offset, int chun
   return proof(to_g1(out.data(), inf));
 }
 
-bool trusted_setup::verify_proof(commit&, proof&, blob& expected_data) {
-  if (expected_data.get_data().size() < 1) throw std::invalid_argument("expected_data size must be 1 or greater");
-  if (expected_data.get_data().size() >= n) return false;
-  throw std::logic_error("verify_proof: the G2 setup / pairing path is not built yet (SURVEY.md 8f rank 3)");
+bool trusted_setup::verify_proof(commit& c, proof& pf, blob& expected_data) {
+  auto& pts = expected_data.get_data();
+  if (pts.size() < 1) throw std::invalid_argument("expected_data size must be 1 or greater");
+  if (pts.size() >= n) return false;
+  const int nl = base_limbs();
+  std::vector<uint64_t> cxy(2 * nl, 0), pxy(2 * nl, 0), xs(4 * pts.size()), ys(4 * pts.size());
+  const G1& cg = c.get_curve_point();
+  const G1& pg = pf.get_curve_point();
+  for (int i = 0; i < nl; i++) {
+    cxy[i] = cg.x[i];
+    cxy[nl + i] = cg.y[i];
+    pxy[i] = pg.x[i];
+    pxy[nl + i] = pg.y[i];
+  }
+  for (size_t j = 0; j < pts.size(); j++) {
+    std::memcpy(&xs[4 * j], pts[j].first.v.data(), 32);
+    std::memcpy(&ys[4 * j], pts[j].second.v.data(), 32);
+  }
+  int ok = 0;
+  check(kzgx_verify_proof(ctx, cxy.data(), cg.inf ? 1 : 0, pxy.data(), pg.inf ? 1 : 0, xs.data(), ys.data(),
+                          pts.size(), &ok),
+        "kzgx_verify_proof");
+  return ok != 0;
 }
 
-void trusted_setup::export_setup(const std::string&) {
-  throw std::logic_error("export_setup: the G2 half of the setup is not built yet (SURVEY.md 8f rank 1)");
+void trusted_setup::export_setup(const std::string& filename) {
+  std::ofstream file(filename, std::ios::out | std::ios::binary | std::ios::trunc);
+  if (!file.is_open()) {
+    std::cerr << "failed to export" << std::endl;
+    return;
+  }
+  const uint64_t num = n;
+  file.write(reinterpret_cast<const char*>(&num), 8);
+  for (const G1& g : g1_points()) {
+    auto rec = ecp_serialize(g);  // u32 len || octet
+    file.write(reinterpret_cast<const char*>(rec.data()), (std::streamsize)rec.size());
+  }
+  for (const G2& g : g2_points()) {
+    auto oct = ecp2_octet(g);
+    const uint32_t len = (uint32_t)oct.size();
+    file.write(reinterpret_cast<const char*>(&len), 4);
+    file.write(reinterpret_cast<const char*>(oct.data()), (std::streamsize)oct.size());
+  }
 }
 
 std::vector<commit> trusted_setup::create_commits(const std::vector<kzg::poly>& polys) {
@@ -460,6 +567,20 @@ std::vector<G1> trusted_setup::g1_points() const {
     bool z = true;
     for (int k = 0; k < 2 * nl; k++) z &= xy[2 * nl * i + k] == 0;
     res.push_back(to_g1(&xy[2 * nl * i], z));
+  }
+  return res;
+}
+
+std::vector<G2> trusted_setup::g2_points() const {
+  const int nl = base_limbs();
+  const size_t n2 = kzgx_srs_g2_size(ctx);
+  std::vector<uint64_t> xy(4 * nl * n2);
+  if (n2) check(kzgx_get_srs_g2(ctx, xy.data(), n2), "kzgx_get_srs_g2");
+  std::vector<G2> res;
+  for (size_t i = 0; i < n2; i++) {
+    bool z = true;
+    for (int k = 0; k < 4 * nl; k++) z &= xy[4 * nl * i + k] == 0;
+    res.push_back(to_g2(&xy[4 * nl * i], z));
   }
   return res;
 }

@@ -5,7 +5,9 @@
 // every commitment / proof is printed and compared bit-for-bit with the
 // golden fixtures by tests/test_gpu_cpp_api.py, and a non-zero exit status
 // on any failed check (the reference never fails its build).
-// verify_proof is not exercised: the pairing path is a later row.
+// verify_proof runs the GPU pairing path (kzgx_verify_proof) on every
+// verify / refute case of testing.cpp:129-252, plus an export_setup -> load
+// round trip (trusted_setup.cpp:76-121, 256-287).
 //
 // usage: test_kzg <curve 0|1> <tau hex> <blob dir>
 #include <kzg.h>
@@ -190,6 +192,138 @@ int main(int argc, char** argv) {
     std::memcpy(junk.data(), &len, 4);
     junk[4] = 4;
     check_test(kzg::commit::deserialize(junk).get_curve_point().inf, "off-curve octet decodes to infinity");
+  }
+
+  // verify_proof: every verify / refute case of testing.cpp:129-252
+  {
+    auto vp = [&](kzg::trusted_setup& k, kzg::commit& c, kzg::proof& p, kzg::blob b) { return k.verify_proof(c, p, b); };
+    {  // empty_verify_test (testing.cpp:139-151)
+      kzg::trusted_setup kzg(128, tau);
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string("some data here"));
+      kzg::commit c = kzg.create_commit(poly);
+      kzg::proof p = kzg.create_proof(poly, 7, 2);
+      check_test(throws([&] { vp(kzg, c, p, kzg::blob::from_string("", 7)); }), "empty verification is invalid");
+    }
+    {  // poly_degree_1_test (testing.cpp:165-190)
+      kzg::trusted_setup kzg(2, tau);
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string("K"));
+      kzg::commit c = kzg.create_commit(poly);
+      kzg::proof p = kzg.create_proof(poly, 0, 1);
+      check_test(vp(kzg, c, p, kzg::blob::from_string("K", 0)), "1 degree polynomial, 1 character proof verification");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("k", 0)), "1 degree polynomial, proof refutation 1");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("jj", 2)), "1 degree polynomial, proof refutation 2");
+    }
+    {  // poly_degree_10_test (testing.cpp:192-220)
+      kzg::trusted_setup kzg(11, tau);
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string("CEBIDAGFJH"));
+      kzg::commit c = kzg.create_commit(poly);
+      kzg::proof p = kzg.create_proof(poly, 2, 3);
+      check_test(vp(kzg, c, p, kzg::blob::from_string("BID", 2)), "10 degree polynomial, proof verification");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("CDEF", 0)), "10 degree polynomial, proof refutation 1");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("CD", 12)), "10 degree polynomial, proof refutation 2");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("BHSDJCSHJDVBZ", 0)), "10 degree polynomial, proof refutation 3");
+    }
+    {  // high_poly_degree_test (testing.cpp:222-252); refutation 4's random string is fixed here
+      kzg::trusted_setup kzg(150, tau);
+      std::string data =
+          "wrgJKdE3t5bECALy3eKIwYxEF3V7Z8KTx0nFe1IX5tjH22F5gXOa5LnIMIQuOiNJj8YL8rqDiZSkZfoEDAmGTXXqqvkCd5WKE2fMtVXa2zKa"
+          "e6opGY4i6bYuUG67LaSXd5tUbO4bNPB0TxnkWrSaQ";
+      kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string(data));
+      kzg::commit c = kzg.create_commit(poly);
+      kzg::proof p = kzg.create_proof(poly, 49, 57);
+      std::string sub = data.substr(49, 57);
+      check_test(vp(kzg, c, p, kzg::blob::from_string(sub, 49)), "149 degree polynomial, proof verification");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string(sub, 50)), "149 degree polynomial, proof refutation 1");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string(data.substr(49, 56), 30)), "149 degree polynomial, proof refutation 2");
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("a", 200)), "149 degree polynomial, proof refutation 3");
+      std::string r200;
+      for (int i = 0; i < 200; i++) r200 += (char)('A' + (i * 7919) % 58);
+      check_test(!vp(kzg, c, p, kzg::blob::from_string(r200, 3)), "149 degree polynomial, proof refutation 4");
+    }
+    {  // chunking_test (testing.cpp:254-286)
+      kzg::trusted_setup kzg(128, tau);
+      unsigned char data[] = "ysudYUGdghv675d";
+      const int cs[3] = {1, 2, 4}, bo[3] = {3, 2, 4}, bl[3] = {9, 10, 8};
+      const char* ex[3] = {"dYUGdghv6", "udYUGdghv6", "YUGdghv6"};
+      for (int t = 0; t < 3; t++) {
+        kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_bytes(data, 0, sizeof(data), cs[t]));
+        kzg::commit c = kzg.create_commit(poly);
+        kzg::proof p = kzg.create_proof(poly, bo[t], bl[t], cs[t]);
+        check_test(vp(kzg, c, p, kzg::blob::from_bytes((const uint8_t*)ex[t], bo[t], bl[t], cs[t])),
+                   "chunking, proof verification for blob" + std::to_string(cs[t]));
+      }
+    }
+    {  // example_test (testing.cpp:104-118): three verifies, one refutation
+      kzg::trusted_setup kzg(128, tau);
+      std::string data = "hello there my name is bob";
+      kzg::poly poly = kzg::poly::deserialize(kzg::poly::from_blob(kzg::blob::from_string(data)).serialize());
+      kzg::commit c = kzg::commit::deserialize(kzg.create_commit(poly).serialize());
+      const int off[3] = {0, 15, 23}, len[3] = {5, 7, 3};
+      for (int t = 0; t < 3; t++) {
+        kzg::proof p = kzg::proof::deserialize(kzg.create_proof(poly, off[t], len[t]).serialize());
+        check_test(vp(kzg, c, p, kzg::blob::from_string(data.substr(off[t], len[t]), off[t])),
+                   "README example, proof verification " + std::to_string(t));
+      }
+      kzg::proof p = kzg.create_proof(poly, 23, 3);
+      check_test(!vp(kzg, c, p, kzg::blob::from_string("alice", 23)), "README example, refutation alice");
+    }
+    {  // eth_blob_test proof verification (testing.cpp:72-76, 96-100) at fixed offsets
+      kzg::trusted_setup kzg(5000, tau);
+      const char* files[2] = {"blob2.txt", "blob1.txt"};
+      const int offs[2] = {10, 100};
+      for (int f = 0; f < 2; f++) {
+        std::ifstream in(dir + "/" + files[f]);
+        std::stringstream buf;
+        buf << in.rdbuf();
+        std::vector<uint8_t> bytes = from_hex(buf.str());
+        int zero_pad = MAX_CHUNK_BYTES - (bytes.size() % MAX_CHUNK_BYTES);
+        for (int i = 0; i < zero_pad; i++) bytes.push_back(0);
+        kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_bytes(bytes.data(), 0, bytes.size(), MAX_CHUNK_BYTES));
+        kzg::commit c = kzg.create_commit(poly);
+        kzg::proof p = kzg.create_proof(poly, offs[f], 4);
+        const int bo = offs[f] * MAX_CHUNK_BYTES;
+        check_test(vp(kzg, c, p, kzg::blob::from_bytes(&bytes[bo], bo, 4 * MAX_CHUNK_BYTES, MAX_CHUNK_BYTES)),
+                   std::string("eth-blob, proof verification for ") + (f ? "blob1" : "blob2"));
+      }
+    }
+  }
+
+  // export_setup -> trusted_setup(filename) round trip (trusted_setup.cpp:76-121, 256-287)
+  {
+    kzg::trusted_setup kzg(40, tau);
+    const std::string path = "/tmp/kzgx_setup_" + std::to_string(kzg::curve()) + ".bin";
+    kzg.export_setup(path);
+    kzg::trusted_setup loaded(path);
+    check_test(loaded.size() == 40, "export/load, size");
+    check_test(loaded.g1_points() == kzg.g1_points() && loaded.g2_points() == kzg.g2_points(),
+               "export/load, identical G1 and G2 points");
+    kzg::poly poly = kzg::poly::from_blob(kzg::blob::from_string("exported setup"));
+    kzg::commit c = loaded.create_commit(poly);
+    check_test(c.get_curve_point() == kzg.create_commit(poly).get_curve_point(), "export/load, same commitment");
+    kzg::proof p = loaded.create_proof(poly, 3, 4);
+    kzg::blob vb = kzg::blob::from_string("orte", 3);
+    check_test(loaded.verify_proof(c, p, vb), "export/load, proof verification");
+    // corrupt one G2 record: the reference throws logic_error (trusted_setup.cpp:116)
+    std::fstream f(path, std::ios::in | std::ios::out | std::ios::binary);
+    const size_t mb = kzg::curve() == KZGX_CURVE_BN254 ? 32 : 48;
+    f.seekp(8 + 40 * (4 + 1 + 2 * mb) + 4 + 1 + 3);
+    f.put((char)0x5a);
+    f.close();
+    bool le = false;
+    try {
+      kzg::trusted_setup bad(path);
+    } catch (const std::logic_error&) {
+      le = true;
+    }
+    check_test(le, "export/load, corrupt G2 record is a logic_error");
+    std::remove(path.c_str());
+    bool re = false;
+    try {
+      kzg::trusted_setup missing(path);
+    } catch (const std::runtime_error&) {
+      re = true;
+    }
+    check_test(re, "load, missing file is a runtime_error");
   }
 
   std::cout << "FAILURES\t" << failures << std::endl;
