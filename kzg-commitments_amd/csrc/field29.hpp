@@ -93,6 +93,17 @@ KZGX_DEV F29<F> f29_sub(const F29<F>& a, const F29<F>& b, const uint32_t (&K)[F:
   return r;
 }
 
+// Modulus limb j as an opaque uniform value.  Left as a literal, a limb that
+// is a power of two (BN254: 2^25) is strength-reduced to a 64-bit shift plus
+// a 64-bit add -- two VALU issues where v_mad_u64_u32 with an SGPR operand
+// is one.  The asm is pure (not volatile), so it is hoisted out of loops.
+template <class F>
+KZGX_DEV uint32_t f29_pl(int j) {
+  uint32_t r;
+  asm("" : "=s"(r) : "0"(F::P[j]));
+  return r;
+}
+
 // Montgomery product a b / R mod m, product scanning; output < 2m when
 // a b < (R / m) m^2 (see header).
 template <class F>
@@ -111,7 +122,7 @@ KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;
@@ -147,7 +158,7 @@ KZGX_DEV F29<F> f29_mul2(const F29<F>& a, const F29<F>& b, const F29<F>& c, cons
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;
@@ -181,7 +192,7 @@ KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * F::P[j];
+      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;

@@ -213,9 +213,12 @@ KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
 }
 
 // waves per SIMD the accumulation kernel is register-budgeted for
+#ifndef KZGX_FIXED_WAVES_BN
+#define KZGX_FIXED_WAVES_BN 3
+#endif
 template <class C>
 constexpr int fixed_accum_waves() {
-  return C::Fp29::L <= 9 ? 3 : 2;
+  return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : 2;
 }
 
 // thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
