@@ -104,6 +104,22 @@ KZGX_DEV uint32_t f29_pl(int j) {
   return r;
 }
 
+// acc += x y as one v_mad_u64_u32.  With KZGX_ASM_MAD each column is a
+// single dependent chain (the compiler cannot re-associate it into two
+// chains that then need a 64-bit merge per column); otherwise plain C.
+KZGX_DEV void mad_vv(uint64_t& acc, uint32_t x, uint32_t y) {
+  acc += (uint64_t)x * y;
+#ifdef KZGX_ASM_MAD
+  asm("" : "+v"(acc));
+#endif
+}
+KZGX_DEV void mad_vs(uint64_t& acc, uint32_t x, uint32_t y_uniform) {
+  acc += (uint64_t)x * y_uniform;
+#ifdef KZGX_ASM_MAD
+  asm("" : "+v"(acc));
+#endif
+}
+
 // Montgomery product a b / R mod m, product scanning; output < 2m when
 // a b < (R / m) m^2 (see header).
 template <class F>
@@ -117,16 +133,16 @@ KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (j >= 0 && j < L) acc += (uint64_t)a.v[i] * b.v[j];
+      if (j >= 0 && j < L) mad_vv(acc, a.v[i], b.v[j]);
     }
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
+      if (i < k && j >= 1 && j < L) mad_vs(acc, q[i], f29_pl<F>(j));
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;
-      acc += (uint64_t)q[k] * F::P[0];
+      mad_vs(acc, q[k], f29_pl<F>(0));
     } else {
       t.v[k - L] = (uint32_t)acc & M29;
     }
@@ -151,18 +167,18 @@ KZGX_DEV F29<F> f29_mul2(const F29<F>& a, const F29<F>& b, const F29<F>& c, cons
     for (int i = 0; i < L; i++) {
       const int j = k - i;
       if (j >= 0 && j < L) {
-        acc += (uint64_t)a.v[i] * b.v[j];
-        acc += (uint64_t)c.v[i] * d.v[j];
+        mad_vv(acc, a.v[i], b.v[j]);
+        mad_vv(acc, c.v[i], d.v[j]);
       }
     }
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
+      if (i < k && j >= 1 && j < L) mad_vs(acc, q[i], f29_pl<F>(j));
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;
-      acc += (uint64_t)q[k] * F::P[0];
+      mad_vs(acc, q[k], f29_pl<F>(0));
     } else {
       t.v[k - L] = (uint32_t)acc & M29;
     }
@@ -186,17 +202,17 @@ KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (j > i && j < L) acc += (uint64_t)a.v[i] * d[j];
+      if (j > i && j < L) mad_vv(acc, a.v[i], d[j]);
     }
-    if ((k & 1) == 0 && (k >> 1) < L) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+    if ((k & 1) == 0 && (k >> 1) < L) mad_vv(acc, a.v[k >> 1], a.v[k >> 1]);
 #pragma unroll
     for (int i = 0; i < L; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < L) acc += (uint64_t)q[i] * f29_pl<F>(j);
+      if (i < k && j >= 1 && j < L) mad_vs(acc, q[i], f29_pl<F>(j));
     }
     if (k < L) {
       q[k] = ((uint32_t)acc * F::INV) & M29;
-      acc += (uint64_t)q[k] * F::P[0];
+      mad_vs(acc, q[k], f29_pl<F>(0));
     } else {
       t.v[k - L] = (uint32_t)acc & M29;
     }
@@ -204,6 +220,19 @@ KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {
   }
   t.v[L - 1] = (uint32_t)acc;
   return t;
+}
+
+// 2m - a for a < m with normalized limbs, no carry chain: one v_sub per
+// limb.  The result (< 2m) has limbs in [0, 2^30), NOT normalized; it may
+// only feed f29_mul / f29_mul2 as one operand (column sums: L 2^59 products
+// + the reduction terms stay < 2^64 for both curves), f29_add / f29_sub
+// (int32 carries absorb limbs < 2^30) or a reduction.
+template <class F>
+KZGX_DEV F29<F> f29_neg_lazy(const F29<F>& a) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = F::P2B[i] - a.v[i];
+  return r;
 }
 
 // a - K if a >= K (K a multiple of m)

@@ -68,6 +68,14 @@ def field29(name, m, L):
     ]
     for k in (2, 4, 6, 8, 10, 16):
         lines.append("  static constexpr uint32_t P%d[L] = %s;  // %dm" % (k, arr29(k * m, L), k))
+    # 2m with every limb borrowed up into [2^29 - 1, 2^30): K - a needs no
+    # carry for any a < m with normalized limbs (lazy negation, field29.hpp)
+    t = limbs29(2 * m, L)
+    b = [t[0] + (1 << 29)] + [t[i] + (1 << 29) - 1 for i in range(1, L - 1)] + [t[L - 1] - 1]
+    assert sum(v << (29 * i) for i, v in enumerate(b)) == 2 * m and all(v < (1 << 30) for v in b)
+    assert b[L - 1] >= (m >> (29 * (L - 1))) and all(v >= (1 << 29) - 1 for v in b[:L - 1])
+    lines.append("  static constexpr uint32_t P2B[L] = {%s};  // 2m, limbs borrowed into [2^29-1, 2^30)" %
+                 ", ".join("0x%08xu" % v for v in b))
     lines += [
         "  static constexpr uint32_t R2[L] = %s;  // R^2 mod m" % arr29(R * R % m, L),
         "  static constexpr uint32_t ONE[L] = %s;  // R mod m" % arr29(R % m, L),

@@ -10,8 +10,8 @@
 //
 //   M[w][i][j] = (j + 1) 2^(c w) P_i      w < W, i < n_t, j < H = 2^(c-1)
 //
-// stored affine, Montgomery form, packed to 2 x 32 B (BN254) / 2 x 48 B
-// (BLS12-381).  A scalar s_i with signed c-bit digits d_w (|d_w| <= H) then
+// stored affine, Montgomery form, as radix-2^29 limbs (80 B BN254 / 112 B
+// BLS12-381, see KZGX_FIXED_L29).  A scalar s_i with signed c-bit digits d_w (|d_w| <= H) then
 // contributes sum_w sign(d_w) M[w][i][|d_w| - 1], so an MSM is a plain sum
 // of n W table points: no bucket sort, no bucket reduction, no doublings.
 // Each thread sums the W terms of ~P points into one XYZZ accumulator with
@@ -19,8 +19,8 @@
 // table lookup for the next term in flight underneath), one wavefront per
 // MSM folds the partials, and one thread per MSM converts to affine.
 //
-// Size: W n_t H points; BN254 c = 15 (W = 17) for the 4097-point prefix of
-// the degree-4096 benchmark is 73 GB -- sized for the 288 GB of HBM3E.
+// Size: W n_t H points; BN254 c = 16 (W = 16) for the 4097-point prefix of
+// the degree-4096 benchmark is 172 GB -- sized for the 288 GB of HBM3E.
 // Every step is an exact group operation, so the affine output is bit-exact
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
@@ -30,10 +30,17 @@
 
 namespace kzgx {
 
-// packed table point: x || y as NW-word little-endian Montgomery residues < m
+// Table point layout.  KZGX_FIXED_L29 (default): x || y as radix-2^29
+// Montgomery limbs exactly as the accumulation kernel consumes them, padded
+// to 16 B (80 B BN254, 112 B BLS12-381) -- no per-term unpacking in the hot
+// loop.  Otherwise: x || y as canonical-width 32-bit words (64 B / 96 B),
+// 12-17% smaller, unpacked per term.
+#ifndef KZGX_FIXED_L29
+#define KZGX_FIXED_L29 1
+#endif
 template <class C>
 constexpr int packed_words() {
-  return 2 * C::Fp::N;
+  return KZGX_FIXED_L29 ? affine_words<C>() : 2 * C::Fp::N;
 }
 
 template <class C, int CB>
@@ -51,6 +58,7 @@ int fixed_windows(int curve, int c) {
 
 template <class C>
 KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
+  if (KZGX_FIXED_L29) return affine_load<C>(p);
   using F = typename C::Fp29;
   constexpr int N = C::Fp::N;
   uint32_t wx[N], wy[N];
@@ -69,6 +77,10 @@ KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
 
 template <class C>
 KZGX_DEV void packed_store(uint32_t* __restrict__ p, const Affine<C>& a) {
+  if (KZGX_FIXED_L29) {
+    affine_store<C>(p, a);
+    return;
+  }
   using F = typename C::Fp29;
   constexpr int N = C::Fp::N;
   uint32_t wx[N], wy[N];
@@ -198,15 +210,29 @@ KZGX_DEV PackedPt<C> packed_fetch(const uint32_t* __restrict__ p) {
 template <class C>
 KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
   using F = typename C::Fp29;
+  Affine<C> a;
+  if (KZGX_FIXED_L29) {
+    constexpr int L = F::L;
+    uint32_t w[packed_words<C>()];
+#pragma unroll
+    for (int k = 0; k < packed_words<C>() / 4; k++) {
+      w[4 * k] = r.q[k].x; w[4 * k + 1] = r.q[k].y; w[4 * k + 2] = r.q[k].z; w[4 * k + 3] = r.q[k].w;
+    }
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      a.x.v[i] = w[i];
+      a.y.v[i] = w[L + i];
+    }
+    return a;
+  }
   constexpr int N = C::Fp::N;
   uint32_t wx[N], wy[N];
 #pragma unroll
   for (int k = 0; k < N / 4; k++) {
-    const uint4 a = r.q[k], b = r.q[N / 4 + k];
-    wx[4 * k] = a.x; wx[4 * k + 1] = a.y; wx[4 * k + 2] = a.z; wx[4 * k + 3] = a.w;
-    wy[4 * k] = b.x; wy[4 * k + 1] = b.y; wy[4 * k + 2] = b.z; wy[4 * k + 3] = b.w;
+    const uint4 p = r.q[k], q = r.q[N / 4 + k];
+    wx[4 * k] = p.x; wx[4 * k + 1] = p.y; wx[4 * k + 2] = p.z; wx[4 * k + 3] = p.w;
+    wy[4 * k] = q.x; wy[4 * k + 1] = q.y; wy[4 * k + 2] = q.z; wy[4 * k + 3] = q.w;
   }
-  Affine<C> a;
   a.x = f29_from_words<F, N>(wx);
   a.y = f29_from_words<F, N>(wy);
   return a;
@@ -262,7 +288,9 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
         nx = packed_fetch<C>(base + (size_t)(w + 1) * wstride + (size_t)((dn < 0 ? -dn : dn) - (dn != 0)) * PW);
       }
       if (d != 0) {
-        if (d < 0) cur = affine_neg<C>(cur);
+        // -T = (x, 2m - y): one v_sub per limb (f29_neg_lazy; the
+        // mixed add only multiplies y and feeds it to carry-absorbing subs)
+        if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
         acc = xyzz_add_affine_impl<C>(acc, cur);
       }
       d = dn;

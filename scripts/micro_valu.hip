@@ -115,6 +115,61 @@ __global__ void k_mov(uint32_t* out, int iters) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+
+// generic 32-bit binary op, 8 independent chains: "OP acc, acc, a"
+#define K_BIN32(NAME, ASM)                                                              \
+  __global__ void NAME(uint32_t* out, int iters) {                                      \
+    uint32_t acc[8];                                                                    \
+    uint32_t a = threadIdx.x + 1;                                                       \
+    for (int k = 0; k < 8; k++) acc[k] = k + 7;                                         \
+    for (int it = 0; it < iters; it++) {                                                \
+      _Pragma("unroll") for (int r = 0; r < REP / 8; r++) {                             \
+        _Pragma("unroll") for (int k = 0; k < 8; k++) asm volatile(ASM : "+v"(acc[k]) : "v"(a)); \
+      }                                                                                 \
+    }                                                                                   \
+    uint32_t s = 0;                                                                     \
+    for (int k = 0; k < 8; k++) s += acc[k];                                            \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                     \
+  }
+K_BIN32(k_add32, "v_add_u32 %0, %0, %1")
+K_BIN32(k_sub32, "v_sub_u32 %0, %0, %1")
+K_BIN32(k_and32, "v_and_b32 %0, %0, %1")
+K_BIN32(k_ashr32, "v_ashrrev_i32 %0, %1, %0")
+K_BIN32(k_align32, "v_alignbit_b32 %0, %0, %1, 11")
+K_BIN32(k_add3, "v_add3_u32 %0, %0, %1, %0")
+K_BIN32(k_mul24, "v_mul_u32_u24 %0, %0, %1")
+K_BIN32(k_mad24, "v_mad_u32_u24 %0, %0, %1, %0")
+
+__global__ void k_lshr64(uint32_t* out, int iters) {
+  uint64_t acc[8];
+  for (int k = 0; k < 8; k++) acc[k] = k + 7 + threadIdx.x;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int r = 0; r < REP / 8; r++) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(acc[k]));
+    }
+  }
+  uint64_t s = 0;
+  for (int k = 0; k < 8; k++) s += acc[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+
+__global__ void k_mov64(uint32_t* out, int iters) {
+  uint64_t acc[8];
+  for (int k = 0; k < 8; k++) acc[k] = k + threadIdx.x;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int r = 0; r < REP / 8; r++) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) asm volatile("v_mov_b64 %0, %1" : "=v"(acc[k]) : "v"(acc[(k + 1) & 7]));
+    }
+  }
+  uint64_t s = 0;
+  for (int k = 0; k < 8; k++) s += acc[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+
 // REP field multiplications per iteration, 4 independent chains per lane
 template <class FP>
 __global__ void k_fe_mul(uint32_t* out, int iters) {
@@ -222,6 +277,16 @@ int main() {
   run(k_addco, "v_add_co_u32", REP, 256, blocks, threads, d_out);
   run(k_lshladd, "v_lshl_add_u64", REP, 256, blocks, threads, d_out);
   run(k_mov, "v_mov_b32", REP, 256, blocks, threads, d_out);
+  run(k_add32, "v_add_u32", REP, 256, blocks, threads, d_out);
+  run(k_sub32, "v_sub_u32", REP, 256, blocks, threads, d_out);
+  run(k_and32, "v_and_b32", REP, 256, blocks, threads, d_out);
+  run(k_ashr32, "v_ashrrev_i32", REP, 256, blocks, threads, d_out);
+  run(k_align32, "v_alignbit_b32", REP, 256, blocks, threads, d_out);
+  run(k_add3, "v_add3_u32", REP, 256, blocks, threads, d_out);
+  run(k_mul24, "v_mul_u32_u24", REP, 256, blocks, threads, d_out);
+  run(k_mad24, "v_mad_u32_u24", REP, 256, blocks, threads, d_out);
+  run(k_lshr64, "v_lshrrev_b64", REP, 256, blocks, threads, d_out);
+  run(k_mov64, "v_mov_b64", REP, 256, blocks, threads, d_out);
   run(k_fe_mul<BN254Fp>, "fe_mul BN254", REP, 4, blocks, threads, d_out);
   run(k_fe_mul<BLS12381Fp>, "fe_mul BLS12381", REP, 2, blocks, threads, d_out);
   run(k_mul29, "mul29 (9 limbs)", REP, 4, blocks, threads, d_out);
