@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
     ap.add_argument("--split", type=int, default=1, help="sub-batches (each on its own stream) per batch")
+    ap.add_argument("--commit-first", action="store_true",
+                    help="enqueue the commit batch before the proof batch (default: proofs first, so the "
+                         "short quotient kernel is dispatched before the commit MSM fills the GPU)")
     ap.add_argument("--cpu-sample", type=int, default=3, help="commits (+ as many proofs) timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -162,12 +165,20 @@ def main():
             lo, hi = cut[s], cut[s + 1]
             if hi == lo:
                 continue
-            if args.workload != "cfg3":
-                ctx.msm_batch_device(d_coeffs[lo].data_ptr(), n, hi - lo, n, d_cout[lo].data_ptr(),
-                                     d_cinf[lo:].data_ptr(), streams[2 * s].cuda_stream)
-            ctx.prove_single_batch_device(d_coeffs[0 if cstride == 0 else lo].data_ptr(), n, cstride,
-                                          d_z[lo].data_ptr(), hi - lo, d_pout[lo].data_ptr(), d_pinf[lo:].data_ptr(),
-                                          d_y[lo].data_ptr(), streams[2 * s + 1].cuda_stream)
+
+            def commits():
+                if args.workload != "cfg3":
+                    ctx.msm_batch_device(d_coeffs[lo].data_ptr(), n, hi - lo, n, d_cout[lo].data_ptr(),
+                                         d_cinf[lo:].data_ptr(), streams[2 * s].cuda_stream)
+
+            def proofs():
+                ctx.prove_single_batch_device(d_coeffs[0 if cstride == 0 else lo].data_ptr(), n, cstride,
+                                              d_z[lo].data_ptr(), hi - lo, d_pout[lo].data_ptr(),
+                                              d_pinf[lo:].data_ptr(), d_y[lo].data_ptr(),
+                                              streams[2 * s + 1].cuda_stream)
+
+            for f in ((commits, proofs) if args.commit_first else (proofs, commits)):
+                f()
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
 
