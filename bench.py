@@ -42,13 +42,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1024, help="polynomials per GPU per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default 1024, cfg3 4096 "
+                         "(BASELINE configs[2]: 4096 openings)")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
     ap.add_argument("--fixed-bits", type=int, default=-1,
-                    help="fixed-base table window (0 = Pippenger only; default 16 BN254 = 137.5 GB, "
-                         "15 BLS12-381 = 116 GB)")
+                    help="fixed-base table window (0 = Pippenger only; default 16: BN254 171.8 GB, "
+                         "BLS12-381 240.6 GB of the 288 GiB HBM)")
     ap.add_argument("--fixed-ppt", type=int, default=16, help="SRS points per accumulation thread (fixed-base path)")
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
@@ -115,12 +117,12 @@ def main():
     tau = K.default_tau(C)
     degree = 4096
     n = degree + 1
-    B = args.batch
+    B = args.batch or (4096 if args.workload == "cfg3" else 1024)
     ctx = kzgx.Context(curve, device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, 5000)
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (16 if curve == "BN254" else 15)
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
     t_setup = time.perf_counter()
     if fixed_bits:
         # precompute the signed-digit multiples of the 4097-point SRS prefix

@@ -180,6 +180,17 @@ int kzgx_pairing(kzgx_ctx* ctx, const uint64_t* g1_xy, const int* g1_inf, const 
  * KZGX_ERR_ARG; needs a G2 setup of >= npoints + 1 points. */
 int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, const uint64_t* proof_xy,
                       int proof_inf, const uint64_t* xs, const uint64_t* ys, size_t npoints, int* ok);
+/* batch of single-point verifies (verify_proof with one opened point each):
+ * ok[k] = e(proof_k, [tau - z_k]G2) == e(commit_k - [y_k]G1, G2), evaluated as
+ * one two-Miller-loop product and one final exponentiation per opening, one
+ * GPU thread each.  Needs G1[0] = G and G2[0..1]; inf arrays may be NULL. */
+int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const int* commit_inf,
+                             const uint64_t* proofs_xy, const int* proof_inf, const uint64_t* zs, const uint64_t* ys,
+                             size_t count, int* ok);
+/* device pointers (inf flags uint32, may be NULL), ok: count x uint32 */
+int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const void* d_commit_inf,
+                                    const void* d_proofs, const void* d_proof_inf, const void* d_z, const void* d_y,
+                                    size_t count, void* d_ok, void* stream);
 
 #ifdef __cplusplus
 }

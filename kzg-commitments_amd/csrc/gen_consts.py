@@ -214,7 +214,9 @@ def g2_data(name):
         digits.append(hard % p)
         hard //= p
     assert hard == 0
-    return dict(p=p, b2=b2, gen=gen, frob=frob, twx=twx, twy=twy, loop=loop, digits=digits, d_type=d_type)
+    z = U if name == "BN254" else X
+    k3 = (X - 1) ** 2 // 3 if name == "BLS12381" else 0
+    return dict(p=p, b2=b2, gen=gen, frob=frob, twx=twx, twy=twy, loop=loop, digits=digits, d_type=d_type, z=z, k3=k3)
 
 
 def pairing_struct(name, L, nw):
@@ -247,6 +249,13 @@ def pairing_struct(name, L, nw):
         "  // (p^4 - p^2 + 1)/r = sum_i HARD[i] p^i (canonical words)",
         "  static constexpr uint32_t HARD[4][%d] = {%s};" % (nw, ", ".join(arr(v, nw) for v in d["digits"])),
         "  static constexpr int HARD_BITS = %d;" % max(v.bit_length() for v in d["digits"]),
+        "  // curve parameter z (BN: u, BLS: x) for the hard part of the final exponentiation",
+        "  static constexpr bool IS_BN = %s;" % ("true" if name == "BN254" else "false"),
+        "  static constexpr uint64_t Z_ABS = 0x%016xull;" % abs(d["z"]),
+        "  static constexpr bool Z_NEG = %s;" % ("true" if d["z"] < 0 else "false"),
+        "  // BLS12: (p^4 - p^2 + 1)/r = K3 (x + p)(x^2 + p^2 - 1) + 1, K3 = (x - 1)^2 / 3",
+        "  static constexpr uint64_t K3[2] = {0x%016xull, 0x%016xull};" % (d["k3"] & (2**64 - 1), d["k3"] >> 64),
+        "  static constexpr int K3_BITS = %d;" % d["k3"].bit_length(),
         "};",
     ]
     return "\n".join(lines)

@@ -661,4 +661,50 @@ int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, 
   return KZGX_OK;
 }
 
+int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const void* d_commit_inf,
+                                    const void* d_proofs, const void* d_proof_inf, const void* d_z, const void* d_y,
+                                    size_t count, void* d_ok, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (count == 0) return KZGX_OK;
+  if (!d_commits || !d_proofs || !d_z || !d_y || !d_ok || count > (1u << 26)) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0 || ctx->n_srs2 < 2) return KZGX_ERR_NO_SRS;
+  return kzgx::verify_single_batch(&ctx->c, (const uint32_t*)d_commits, (const uint32_t*)d_commit_inf,
+                                   (const uint32_t*)d_proofs, (const uint32_t*)d_proof_inf, (const uint32_t*)d_z,
+                                   (const uint32_t*)d_y, count, ctx->d_srs_canon, ctx->d_srs2_canon,
+                                   (uint32_t*)d_ok, pick(ctx, stream));
+}
+
+int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const int* commit_inf,
+                             const uint64_t* proofs_xy, const int* proof_inf, const uint64_t* zs, const uint64_t* ys,
+                             size_t count, int* ok) {
+  KZGX_TRY(activate(ctx));
+  if (count == 0) return KZGX_OK;
+  if (!commits_xy || !proofs_xy || !zs || !ys || !ok || count > (1u << 26)) return KZGX_ERR_ARG;
+  const size_t pb = point_words(ctx) * 4;
+  void *d_c, *d_p, *d_s, *d_f;
+  KZGX_TRY(stage(ctx, 0, count * pb, &d_c));
+  KZGX_TRY(stage(ctx, 1, count * pb, &d_p));
+  KZGX_TRY(stage(ctx, 2, count * 64, &d_s));
+  KZGX_TRY(stage(ctx, 3, count * 12, &d_f));
+  std::vector<uint32_t> fl(2 * count);
+  for (size_t k = 0; k < count; k++) {
+    fl[k] = commit_inf ? (uint32_t)(commit_inf[k] != 0) : 0u;
+    fl[count + k] = proof_inf ? (uint32_t)(proof_inf[k] != 0) : 0u;
+  }
+  hipStream_t st = ctx->c.stream;
+  KZGX_TRY_HIP(hipMemcpyAsync(d_c, commits_xy, count * pb, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_p, proofs_xy, count * pb, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_s, zs, count * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync((char*)d_s + count * 32, ys, count * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_f, fl.data(), count * 8, hipMemcpyHostToDevice, st));
+  uint32_t* d_ok = (uint32_t*)d_f + 2 * count;
+  KZGX_TRY(kzgx_verify_single_batch_device(ctx, d_c, d_f, d_p, (uint32_t*)d_f + count, d_s,
+                                           (char*)d_s + count * 32, count, d_ok, nullptr));
+  std::vector<uint32_t> v(count);
+  KZGX_TRY_HIP(hipMemcpyAsync(v.data(), d_ok, count * 4, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  for (size_t k = 0; k < count; k++) ok[k] = (int)v[k];
+  return KZGX_OK;
+}
+
 }  // extern "C"

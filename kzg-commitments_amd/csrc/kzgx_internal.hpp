@@ -166,6 +166,9 @@ int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n
 int g2_validate(Ctx* ctx, const uint32_t* d_xy, size_t count, uint32_t* d_ok, hipStream_t st);
 int pairing_batch(Ctx* ctx, const uint32_t* d_g1, const uint32_t* d_g1_inf, const uint32_t* d_g2,
                   const uint32_t* d_g2_inf, size_t count, uint32_t* d_out, hipStream_t st);
+int verify_single_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
+                        const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
+                        const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_ok, hipStream_t st);
 int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 

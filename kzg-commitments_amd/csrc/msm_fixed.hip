@@ -242,9 +242,12 @@ KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
 #ifndef KZGX_FIXED_WAVES_BN
 #define KZGX_FIXED_WAVES_BN 3
 #endif
+#ifndef KZGX_FIXED_WAVES_BLS
+#define KZGX_FIXED_WAVES_BLS 2
+#endif
 template <class C>
 constexpr int fixed_accum_waves() {
-  return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : 2;
+  return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : KZGX_FIXED_WAVES_BLS;
 }
 
 // thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...

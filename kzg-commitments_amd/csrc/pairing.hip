@@ -7,9 +7,10 @@
 // functions evaluated at P and placed as sparse Fp12 elements, then the
 // exact final exponentiation f^((p^12 - 1)/r):
 //   easy part   f^(p^6 - 1)(p^2 + 1)       (conjugate, inverse, Frobenius)
-//   hard part   f^((p^4 - p^2 + 1)/r), written in base p as
-//               sum_i HARD[i] p^i, so f^hard = prod_i frob^i(f)^HARD[i],
-//               one joint square-and-multiply over a 16-entry table.
+//   hard part   f^((p^4 - p^2 + 1)/r) through exact curve-parameter
+//               chains with cyclotomic (Granger-Scott) squarings: BN254
+//               via l0 + l1 p + l2 p^2 + p^3 in u (Scott et al.), BLS12-381
+//               via K3 (x + p)(x^2 + p^2 - 1) + 1, K3 = (x - 1)^2 / 3.
 // BN254 (miracl Nogami, u < 0, D-type twist): loop |6u + 2|, then
 // conjugate (u < 0), then the two Frobenius lines l_{T, pi(Q)},
 // l_{T + pi(Q), -pi^2(Q)}.  BLS12-381 (x < 0, M-type twist): loop |x|, then
@@ -114,31 +115,101 @@ KZGX_TW Fp12<C> miller_loop(const Affine<C>& p, const G2A<C>& q) {
   return f;
 }
 
+// Granger-Scott squaring, valid in the cyclotomic subgroup (after the easy
+// part): three Fp4 squarings, 6 Fp2 products instead of 18
+template <class C>
+KZGX_DEV void fp4_sqr(const Fp2<C>& a, const Fp2<C>& b, Fp2<C>& c0, Fp2<C>& c1) {
+  // (a + b y)^2 with y^2 = xi: c0 = a^2 + xi b^2, c1 = 2 a b
+  const Fp2<C> t = f2_mul<C>(a, b);
+  c0 = f2_sub<C>(f2_sub<C>(f2_mul<C>(f2_add<C>(a, b), f2_add<C>(a, f2_mul_xi<C>(b))), t), f2_mul_xi<C>(t));
+  c1 = f2_dbl<C>(t);
+}
+template <class C>
+KZGX_TW Fp12<C> f12_cyclo_sqr(const Fp12<C>& f) {
+  Fp2<C> z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  Fp2<C> t0, t1, t2, t3, t4, t5;
+  fp4_sqr<C>(z0, z1, t0, t1);
+  fp4_sqr<C>(z2, z3, t2, t3);
+  fp4_sqr<C>(z4, z5, t4, t5);
+  z0 = f2_sub<C>(t0, z0);
+  z0 = f2_add<C>(f2_dbl<C>(z0), t0);
+  z1 = f2_add<C>(t1, z1);
+  z1 = f2_add<C>(f2_dbl<C>(z1), t1);
+  const Fp2<C> x5 = f2_mul_xi<C>(t5);
+  z2 = f2_add<C>(x5, z2);
+  z2 = f2_add<C>(f2_dbl<C>(z2), x5);
+  z3 = f2_sub<C>(t4, z3);
+  z3 = f2_add<C>(f2_dbl<C>(z3), t4);
+  z4 = f2_sub<C>(t2, z4);
+  z4 = f2_add<C>(f2_dbl<C>(z4), t2);
+  z5 = f2_add<C>(t3, z5);
+  z5 = f2_add<C>(f2_dbl<C>(z5), t3);
+  Fp12<C> r;
+  r.c0.c0 = z0;
+  r.c0.c1 = z4;
+  r.c0.c2 = z3;
+  r.c1.c0 = z2;
+  r.c1.c1 = z1;
+  r.c1.c2 = z5;
+  return r;
+}
+
+// f^e for f in the cyclotomic subgroup, e = (e[1]:e[0]) of `bits` bits
+template <class C>
+KZGX_TW Fp12<C> cyclo_pow(const Fp12<C>& f, uint64_t e0, uint64_t e1, int bits) {
+  Fp12<C> acc = f;
+  for (int i = bits - 2; i >= 0; i--) {
+    acc = f12_cyclo_sqr<C>(acc);
+    if (((i < 64 ? e0 >> i : e1 >> (i - 64)) & 1ull)) acc = f12_mul<C>(acc, f);
+  }
+  return acc;
+}
+
+// f^z for the curve parameter z (BN: u, BLS: x); z < 0 -> unitary inverse
+template <class C>
+KZGX_DEV Fp12<C> cyclo_pow_z(const Fp12<C>& f) {
+  using P = typename PairOf<C>::T;
+  constexpr int bits = 64 - __builtin_clzll(P::Z_ABS);
+  const Fp12<C> r = cyclo_pow<C>(f, P::Z_ABS, 0, bits);
+  return P::Z_NEG ? f12_conj<C>(r) : r;
+}
+
+// g^n for a small constant n >= 1 (cyclotomic g)
+template <class C>
+KZGX_DEV Fp12<C> cyclo_pow_small(const Fp12<C>& g, uint32_t n) {
+  return cyclo_pow<C>(g, n, 0, 32 - __builtin_clz(n));
+}
+
+// exact final exponentiation f^((p^12 - 1)/r)
 template <class C>
 KZGX_TW Fp12<C> final_exp(const Fp12<C>& f) {
   using P = typename PairOf<C>::T;
-  // easy part: f^(p^6 - 1) (p^2 + 1)
+  // easy part: f^(p^6 - 1) (p^2 + 1) -> cyclotomic subgroup
   Fp12<C> g = f12_mul<C>(f12_conj<C>(f), f12_inv<C>(f));
   g = f12_mul<C>(f12_frob<C>(f12_frob<C>(g)), g);
-  // hard part: prod_i frob^i(g)^HARD[i]
-  Fp12<C> tab[16];
-  Fp12<C> b[4];
-  b[0] = g;
-  for (int i = 1; i < 4; i++) b[i] = f12_frob<C>(b[i - 1]);
-  tab[0] = f12_one<C>();
-  for (int m = 1; m < 16; m++) {
-    const int low = __builtin_ctz(m);
-    const int rest = m & (m - 1);
-    tab[m] = rest ? f12_mul<C>(tab[rest], b[low]) : b[low];
+  if (P::IS_BN) {
+    // (p^4 - p^2 + 1)/r = l0 + l1 p + l2 p^2 + p^3 (exact, Scott et al.):
+    //   l2 = 6u^2 + 1, l1 = -36u^3 - 18u^2 - 12u + 1, l0 = -36u^3 - 30u^2 - 18u - 2
+    const Fp12<C> a = cyclo_pow_z<C>(g);  // g^u
+    const Fp12<C> b = cyclo_pow_z<C>(a);  // g^(u^2)
+    const Fp12<C> c = cyclo_pow_z<C>(b);  // g^(u^3)
+    const Fp12<C> c36 = cyclo_pow_small<C>(c, 36);
+    const Fp12<C> g2 = f12_cyclo_sqr<C>(g);
+    const Fp12<C> f0 = f12_conj<C>(f12_mul<C>(f12_mul<C>(c36, cyclo_pow_small<C>(b, 30)),
+                                              f12_mul<C>(cyclo_pow_small<C>(a, 18), g2)));
+    const Fp12<C> f1 =
+        f12_mul<C>(f12_conj<C>(f12_mul<C>(c36, f12_mul<C>(cyclo_pow_small<C>(b, 18), cyclo_pow_small<C>(a, 12)))), g);
+    const Fp12<C> f2 = f12_mul<C>(cyclo_pow_small<C>(b, 6), g);
+    Fp12<C> r = f12_mul<C>(f0, f12_frob<C>(f1));
+    r = f12_mul<C>(r, f12_frob<C>(f12_frob<C>(f2)));
+    return f12_mul<C>(r, f12_frob<C>(f12_frob<C>(f12_frob<C>(g))));
   }
-  Fp12<C> acc = f12_one<C>();
-  for (int bit = P::HARD_BITS - 1; bit >= 0; bit--) {
-    acc = f12_sqr<C>(acc);
-    int idx = 0;
-    for (int i = 0; i < 4; i++) idx |= (int)((P::HARD[i][bit >> 5] >> (bit & 31)) & 1u) << i;
-    if (idx) acc = f12_mul<C>(acc, tab[idx]);
-  }
-  return acc;
+  // BLS12: (p^4 - p^2 + 1)/r = K3 (x + p)(x^2 + p^2 - 1) + 1, K3 = (x - 1)^2 / 3
+  const Fp12<C> t = cyclo_pow<C>(g, P::K3[0], P::K3[1], P::K3_BITS);
+  const Fp12<C> t2 = f12_mul<C>(cyclo_pow_z<C>(t), f12_frob<C>(t));  // t^(x + p)
+  const Fp12<C> t3 = f12_mul<C>(f12_mul<C>(cyclo_pow_z<C>(cyclo_pow_z<C>(t2)), f12_frob<C>(f12_frob<C>(t2))),
+                                f12_conj<C>(t2));  // t2^(x^2 + p^2 - 1)
+  return f12_mul<C>(t3, g);
 }
 
 // thread per pairing: e(P_k, Q_k) for canonical affine inputs (all-zero or
@@ -262,6 +333,68 @@ __global__ void k_g1_sub(const uint32_t* __restrict__ a, const uint32_t* __restr
   *out_inf = fin ? 0u : 1u;
 }
 
+// ---- batched single-point verify -----------------------------------------------
+// [k] P for a canonical 256-bit scalar (XYZZ double-and-add, complete)
+template <class C>
+KZGX_TW Xyzz<C> g1_mul_words(const Affine<C>& p, const uint32_t (&e)[8]) {
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (int b = 255; b >= 0; b--) {
+    acc = xyzz_dbl<C>(acc);
+    if ((e[b >> 5] >> (b & 31)) & 1u) acc = xyzz_add_affine<C>(acc, p);
+  }
+  return acc;
+}
+
+// thread per opening: verify_proof with one point (x = z, y), i.e.
+//   e(pi, [tau - z]G2) == e(C - [y]G1, G2)
+//   <=> e(pi, [tau]G2) * e(-(C - [y]G1 + [z]pi), G2) == 1,
+// one product of two Miller loops and ONE final exponentiation.  The
+// boolean is that of the reference (trusted_setup.cpp:230-254 with
+// I = y, Z = X - z).  G1[0] = G, G2[0] = G2, G2[1] = [tau]G2 from the setup.
+template <class C>
+__global__ __launch_bounds__(64) void k_verify_single(const uint32_t* __restrict__ commits,
+                                                      const uint32_t* __restrict__ commit_inf,
+                                                      const uint32_t* __restrict__ proofs,
+                                                      const uint32_t* __restrict__ proof_inf,
+                                                      const uint32_t* __restrict__ zs, const uint32_t* __restrict__ ys,
+                                                      uint32_t count, const uint32_t* __restrict__ g1_0,
+                                                      const uint32_t* __restrict__ g2_01, uint32_t* __restrict__ ok) {
+  constexpr int N = C::Fp::N;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  Affine<C> c, pi, g;
+  const bool cf = affine_from_canonical<C>(commits + (size_t)k * 2 * N, c) && !(commit_inf && commit_inf[k]);
+  const bool pf = affine_from_canonical<C>(proofs + (size_t)k * 2 * N, pi) && !(proof_inf && proof_inf[k]);
+  const bool gf = affine_from_canonical<C>(g1_0, g);
+  uint32_t zw[8], yw[8];
+  for (int i = 0; i < 8; i++) {
+    zw[i] = zs[(size_t)k * 8 + i];
+    yw[i] = ys[(size_t)k * 8 + i];
+  }
+  // D = C - [y]G + [z]pi
+  Xyzz<C> d = xyzz_inf<C>();
+  if (gf) d = xyzz_neg<C>(g1_mul_words<C>(g, yw));
+  if (cf) d = xyzz_add_affine<C>(d, c);
+  if (pf) d = xyzz_add<C>(d, g1_mul_words<C>(pi, zw));
+  Affine<C> dn;
+  const bool df = xyzz_to_affine<C>(d, dn);
+  G2A<C> g2, tg2;
+  const bool g2f = g2_from_canon<C>(g2_01, g2);
+  const bool tg2f = g2_from_canon<C>(g2_01 + 4 * N, tg2);
+  Fp12<C> f = f12_one<C>();
+  if (pf && tg2f) f = miller_loop<C>(pi, tg2);
+  if (df && g2f) {
+    dn = affine_neg<C>(dn);
+    f = f12_mul<C>(f, miller_loop<C>(dn, g2));
+  }
+  const Fp12<C> e = final_exp<C>(f);
+  uint32_t w[12 * N];
+  f12_to_canon<C>(e, w);
+  uint32_t bad = w[0] ^ 1u;  // == 1 in Fp12: coefficient 0 is 1, all others 0
+  for (int i = 1; i < 12 * N; i++) bad |= w[i];
+  ok[k] = bad == 0 ? 1u : 0u;
+}
+
 // ---- host side ----------------------------------------------------------------
 template <class C>
 static int pairing_impl(const uint32_t* g1, const uint32_t* g1_inf, const uint32_t* g2, const uint32_t* g2_inf,
@@ -327,6 +460,22 @@ int g2_validate(Ctx* ctx, const uint32_t* d_xy, size_t count, uint32_t* d_ok, hi
     hipLaunchKernelGGL(k_g2_validate<BN254G1>, grd, blk, 0, st, d_xy, (uint32_t)count, d_ok);
   else
     hipLaunchKernelGGL(k_g2_validate<BLS12381G1>, grd, blk, 0, st, d_xy, (uint32_t)count, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int verify_single_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
+                        const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
+                        const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_ok, hipStream_t st) {
+  if (count == 0) return KZGX_OK;
+  dim3 blk(64), grd((unsigned)((count + 63) / 64));
+  ProfScope p(ctx, st, "verify_single");
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_verify_single<BN254G1>, grd, blk, 0, st, d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z,
+                       d_y, (uint32_t)count, d_g1_0, d_g2_01, d_ok);
+  else
+    hipLaunchKernelGGL(k_verify_single<BLS12381G1>, grd, blk, 0, st, d_commits, d_commit_inf, d_proofs, d_proof_inf,
+                       d_z, d_y, (uint32_t)count, d_g1_0, d_g2_01, d_ok);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }

@@ -27,7 +27,8 @@ EXPORTS = [
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
-    "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof",
+    "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
+    "kzgx_verify_single_batch_device",
 ]
 
 _lib = None
@@ -89,6 +90,8 @@ def lib():
             "kzgx_msm_g2": (ctypes.c_int, [vp, u64p, sz, u64p, intp]),
             "kzgx_pairing": (ctypes.c_int, [vp, u64p, intp, u64p, intp, sz, u64p]),
             "kzgx_verify_proof": (ctypes.c_int, [vp, u64p, ctypes.c_int, u64p, ctypes.c_int, u64p, u64p, sz, intp]),
+            "kzgx_verify_single_batch": (ctypes.c_int, [vp, u64p, intp, u64p, intp, u64p, u64p, sz, intp]),
+            "kzgx_verify_single_batch_device": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, sz, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -339,3 +342,22 @@ class Context:
                                      _p(x) if x.shape[0] else None, _p(y) if y.shape[0] else None, x.shape[0],
                                      ctypes.byref(ok)), "kzgx_verify_proof")
         return bool(ok.value)
+
+    def verify_single_batch(self, commits, proofs, zs, ys, commit_inf=None, proof_inf=None) -> np.ndarray:
+        c = np.ascontiguousarray(commits, dtype=np.uint64).reshape(-1, 2 * self.w64)
+        p = np.ascontiguousarray(proofs, dtype=np.uint64).reshape(-1, 2 * self.w64)
+        z, y = as_scalars(zs), as_scalars(ys)
+        n = c.shape[0]
+        assert p.shape[0] == n and z.shape[0] == n and y.shape[0] == n
+        fc = None if commit_inf is None else np.ascontiguousarray(commit_inf, dtype=np.int32)
+        fp = None if proof_inf is None else np.ascontiguousarray(proof_inf, dtype=np.int32)
+        ok = np.zeros(n, dtype=np.int32)
+        _chk(lib().kzgx_verify_single_batch(self.h, _p(c), None if fc is None else fc.ctypes.data_as(intp), _p(p),
+                                            None if fp is None else fp.ctypes.data_as(intp), _p(z), _p(y), n,
+                                            ok.ctypes.data_as(intp)), "kzgx_verify_single_batch")
+        return ok.astype(bool)
+
+    def verify_single_batch_device(self, d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y, count, d_ok,
+                                   stream=None):
+        _chk(lib().kzgx_verify_single_batch_device(self.h, d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y,
+                                                   count, d_ok, stream), "kzgx_verify_single_batch_device")

@@ -224,3 +224,43 @@ def test_verify_proof_degenerate_setups(name, C, ctxs):
         assert ctx.verify_proof(com, cinf, prf, pinf, scalars(xs), scalars(ys))
         ys[0] = (ys[0] + 7) % C.r
         assert not ctx.verify_proof(com, cinf, prf, pinf, scalars(xs), scalars(ys))
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_verify_single_batch(name, C, ctxs):
+    """batched single-point verifies == verify_proof(commit, proof, {(z, y)})
+    (reference trusted_setup.cpp:230-254 with one point), against the
+    known-tau oracle on valid and tampered openings"""
+    ctx = ctxs(name)
+    tau = K.default_tau(C)
+    _setup(ctx, C, tau, 64)
+    polys = [K.random_scalars(C, 40, seed=100 + i) for i in range(3)] + [[0] * 40]
+    zs, ys, cs, cis, ps, pis, exp = [], [], [], [], [], [], []
+    for j, P in enumerate(polys):
+        S = scalars(P)
+        com, cinf = ctx.msm(S)
+        pts = [5, 17, C.r - 3, 0]
+        prf, pinf, yv = ctx.prove_single_batch(S, scalars(pts))
+        for t, z in enumerate(pts):
+            y = to_int(yv[t])
+            for mode in ("ok", "bad_y", "bad_z", "bad_c"):
+                zz, yy, cc, ci = z, y, com, cinf
+                if mode == "bad_y":
+                    yy = (y + 1) % C.r
+                elif mode == "bad_z":
+                    zz = (z + 1) % C.r
+                elif mode == "bad_c":
+                    cc, ci = prf[t], pinf[t]  # a different group element in the commit slot
+                zs.append(zz)
+                ys.append(yy)
+                cs.append(cc)
+                cis.append(int(ci))
+                ps.append(prf[t])
+                pis.append(int(pinf[t]))
+                cP = None if ci else (to_int(cc[:w64(C)]), to_int(cc[w64(C):]))
+                pP = None if pinf[t] else (to_int(prf[t][:w64(C)]), to_int(prf[t][w64(C):]))
+                exp.append(K.verify_proof_tau(C, tau, 64, cP, pP, [(zz, yy)]))
+    got = ctx.verify_single_batch(np.stack(cs), np.stack(ps), scalars(zs), scalars(ys), commit_inf=cis,
+                                  proof_inf=pis)
+    assert got.tolist() == exp
+    assert sum(exp) >= 16  # the valid openings (and the zero polynomial's degenerate ones)
