@@ -171,6 +171,10 @@ class trusted_setup {
   /** Extensions: batched commits / single-point openings in one GPU pass. */
   std::vector<commit> create_commits(const std::vector<kzg::poly>& polys);
   std::vector<proof> create_proofs(const kzg::poly& poly, const std::vector<long>& points);
+  /** Extension: many single-point verify_proof calls in one GPU pass;
+   *  result k == verify_proof(commits[k], proofs[k], blob {points[k]}). */
+  std::vector<bool> verify_proofs(std::vector<commit>& commits, std::vector<proof>& proofs,
+                                  const std::vector<std::pair<Fr, Fr>>& points);
   /** copy of the G1 / G2 SRS points */
   std::vector<G1> g1_points() const;
   std::vector<G2> g2_points() const;

@@ -558,6 +558,35 @@ std::vector<proof> trusted_setup::create_proofs(const kzg::poly& p, const std::v
   return res;
 }
 
+std::vector<bool> trusted_setup::verify_proofs(std::vector<commit>& commits, std::vector<proof>& proofs,
+                                              const std::vector<std::pair<Fr, Fr>>& points) {
+  const size_t m = commits.size();
+  if (proofs.size() != m || points.size() != m) throw std::invalid_argument("verify_proofs: size mismatch");
+  std::vector<bool> res(m, false);
+  if (m == 0) return res;
+  const int nl = base_limbs();
+  std::vector<uint64_t> c(2 * nl * m, 0), p(2 * nl * m, 0), z(4 * m), y(4 * m);
+  std::vector<int> ci(m), pi(m), ok(m);
+  for (size_t k = 0; k < m; k++) {
+    const G1& cg = commits[k].get_curve_point();
+    const G1& pg = proofs[k].get_curve_point();
+    for (int i = 0; i < nl; i++) {
+      c[2 * nl * k + i] = cg.x[i];
+      c[2 * nl * k + nl + i] = cg.y[i];
+      p[2 * nl * k + i] = pg.x[i];
+      p[2 * nl * k + nl + i] = pg.y[i];
+    }
+    ci[k] = cg.inf;
+    pi[k] = pg.inf;
+    std::memcpy(&z[4 * k], points[k].first.v.data(), 32);
+    std::memcpy(&y[4 * k], points[k].second.v.data(), 32);
+  }
+  check(kzgx_verify_single_batch(ctx, c.data(), ci.data(), p.data(), pi.data(), z.data(), y.data(), m, ok.data()),
+        "kzgx_verify_single_batch");
+  for (size_t k = 0; k < m; k++) res[k] = ok[k] != 0;
+  return res;
+}
+
 std::vector<G1> trusted_setup::g1_points() const {
   const int nl = base_limbs();
   std::vector<uint64_t> xy(2 * nl * n);

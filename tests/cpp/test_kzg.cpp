@@ -183,6 +183,29 @@ int main(int argc, char** argv) {
     auto prs = kzg.create_proofs(ps[4], {0, 3, 184});
     same = prs[1].get_curve_point() == kzg.create_proof(ps[4], 3, 1).get_curve_point();
     check_test(same, "create_proofs == create_proof");
+    // batched single-point verifies agree with verify_proof, valid and refuted
+    std::vector<kzg::commit> vc;
+    std::vector<kzg::proof> vpf;
+    std::vector<std::pair<kzg::Fr, kzg::Fr>> pts;
+    std::string s4(37 * 5, 'e');
+    const long zz[3] = {0, 3, 184};
+    for (int t = 0; t < 3; t++) {
+      kzg::blob b = kzg::blob::from_string(s4.substr(zz[t], 1), (int)zz[t]);
+      pts.push_back(b.get_data()[0]);
+      vc.push_back(cs[4]);
+      vpf.push_back(prs[t]);
+    }
+    pts.push_back({kzg::Fr(3L), kzg::Fr(5L)});  // wrong value at x = 3
+    vc.push_back(cs[4]);
+    vpf.push_back(prs[1]);
+    auto vr = kzg.verify_proofs(vc, vpf, pts);
+    bool agree = vr.size() == 4 && vr[0] && vr[1] && vr[2] && !vr[3];
+    for (int t = 0; t < 4 && agree; t++) {
+      std::vector<std::pair<kzg::Fr, kzg::Fr>> one = {pts[t]};
+      kzg::blob b(one);
+      agree = kzg.verify_proof(vc[t], vpf[t], b) == vr[t];
+    }
+    check_test(agree, "verify_proofs == verify_proof (3 valid, 1 refuted)");
   }
 
   // bad octets deserialize to infinity (util.cpp:107-112)
