@@ -308,6 +308,23 @@ def main():
                     traffic = tj.get("msm_accum_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
+        valu = None
+        vpath = os.path.join(ROOT, "profiles", "pmc_valu_cfg2.json")
+        if os.path.exists(vpath) and acc_cnt and curve == "BN254":
+            try:
+                with open(vpath) as f:
+                    vj = json.load(f)
+                # VALU issue roofline of the accumulation kernel: PMC instruction
+                # count per MSM x MSMs per launch / live launch time, against
+                # 1024 SIMDs x 2.4 GHz / (measured mix cost per instruction)
+                ipl = vj["valu_insts_per_launch"] * B / vj["batch"]  # one launch = B MSMs of ~4097 points
+                rate = ipl / (avg_launch_ms * 1e-3)
+                peak = 256 * 4 * 2.4e9 / vj["mix_cost_cycles_per_inst"]
+                valu = {"wave_insts_per_s": rate, "peak_wave_insts_per_s": peak, "frac": rate / peak,
+                        "insts_per_wave_mixed_add": vj["valu_insts_per_wave_mixed_add"],
+                        "source": "profiles/pmc_valu_cfg2.json (PMC SQ_INSTS_VALU) + live launch time"}
+            except (OSError, ValueError, KeyError):
+                valu = None
         total_units = units_per_step * args.steps * world
         value = total_units / elapsed
         if fb[0]:
@@ -360,6 +377,7 @@ def main():
                 "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
                 "event_ms_total": ev_ms,
                 "fixed_table_setup_s": t_setup if fb[0] else None,
+                "valu_roofline": valu,
             },
             "parity": {"checked": checked, "ok": int(ok), "method": "[P(tau)]G1 / [q(tau)]G1 identity"},
             "cpu_baseline": cpu,
