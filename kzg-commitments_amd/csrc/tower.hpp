@@ -16,6 +16,14 @@
 #include "curve.hpp"
 
 #define KZGX_TW __device__ __noinline__
+// Fp2 products: inlined into their (non-inlined) Fp6 / G2 callers by
+// default -- a call per Fp2 product costs more in argument copies and
+// callee-saved spills than the product itself on single-lane pairing code
+#ifndef KZGX_F2_NOINLINE
+#define KZGX_TW2 __device__ __forceinline__
+#else
+#define KZGX_TW2 __device__ __noinline__
+#endif
 
 namespace kzgx {
 
@@ -121,7 +129,7 @@ KZGX_DEV Fp2<C> f2_dbl(const Fp2<C>& x) {
   return f2_add<C>(x, x);
 }
 template <class C>
-KZGX_TW Fp2<C> f2_mul(const Fp2<C>& x, const Fp2<C>& y) {
+KZGX_TW2 Fp2<C> f2_mul(const Fp2<C>& x, const Fp2<C>& y) {
   using F = typename C::Fp29;
   const F29<F> t0 = f29_mul<F>(x.a, y.a);
   const F29<F> t1 = f29_mul<F>(x.b, y.b);
@@ -130,7 +138,7 @@ KZGX_TW Fp2<C> f2_mul(const Fp2<C>& x, const Fp2<C>& y) {
   return Fp2<C>{fp_sub<F>(t0, t1), fp_sub<F>(fp_sub<F>(t2, t0), t1)};
 }
 template <class C>
-KZGX_TW Fp2<C> f2_sqr(const Fp2<C>& x) {
+KZGX_TW2 Fp2<C> f2_sqr(const Fp2<C>& x) {
   using F = typename C::Fp29;
   // (a + b)(a - b), 2 a b
   const F29<F> c0 = f29_mul<F>(f29_add<F>(x.a, x.b), fp_sub<F>(x.a, x.b));
