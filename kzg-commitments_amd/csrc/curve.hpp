@@ -27,6 +27,15 @@
 // time) without helping the scheduler.  The hot loop uses the _impl forms.
 #define KZGX_PT __device__ __noinline__
 
+// -Y1 in the mixed add's Y3: carry-free 8m - Y1 (f29_neg8_lazy) or the
+// carried 4m - Y1.  The lazy form saves ~25 VALU instructions but makes the
+// compiler spill around the rare P == +-a branch of the fixed-base kernel.
+#ifdef KZGX_LAZY_NEG_Y1
+#define KZGX_NEG_Y1(y) f29_neg8_lazy<F>(y)
+#else
+#define KZGX_NEG_Y1(y) f29_sub<F>(f29_zero<F>(), (y), F::P4)
+#endif
+
 namespace kzgx {
 
 template <class C>
@@ -127,7 +136,15 @@ KZGX_DEV Xyzz<C> xyzz_dbl_impl(const Xyzz<C>& p) {
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
   using F = typename C::Fp29;
+#ifdef KZGX_LAZY_NEG_Y1
+  if (xyzz_is_inf<C>(p)) {  // keep Y normalized (a.y may be a lazy negation)
+    Xyzz<C> r = xyzz_from_affine<C>(a);
+    r.Y = f29_normalize<F>(a.y);
+    return r;
+  }
+#else
   if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
+#endif
   F29<F> U2 = f29_mul<F>(a.x, p.ZZ);                    // < 2m
   F29<F> S2 = f29_mul<F>(a.y, p.ZZZ);                   // < 2m
   F29<F> P = f29_sub<F>(U2, p.X, F::P8);                // < 10m
@@ -140,9 +157,12 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
   F29<F> PPP = f29_mul<F>(P, PP);
   F29<F> Q = f29_mul<F>(p.X, PP);
   Xyzz<C> r;
-  r.X = f29_sub<F>(f29_sqr<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);       // < 8m
-  // R (Q - X3) - Y1 PPP with one reduction: < 60m^2 + 8m^2 -> < 2m
-  r.Y = f29_mul2<F>(R, f29_sub<F>(Q, r.X, F::P8), f29_sub<F>(f29_zero<F>(), p.Y, F::P4), PPP);
+  // PPP + 2Q < 6m without carries (limbs < 3 2^29): f29_sub absorbs them
+  r.X = f29_sub<F>(f29_sqr<F>(R), f29_add_2x_lazy<F>(PPP, Q), F::P6);       // < 8m
+  // R (Q - X3) - Y1 PPP with one reduction: < 60m^2 + 16m^2 -> < 2m.  8m - Y1
+  // is carry-free (limbs < 2^30; Y1 < 4m normalized: every path writes Y
+  // normalized); the column sums hold with it as the one lazy operand.
+  r.Y = f29_mul2<F>(R, f29_sub<F>(Q, r.X, F::P8), KZGX_NEG_Y1(p.Y), PPP);
   r.ZZ = f29_mul<F>(p.ZZ, PP);
   r.ZZZ = f29_mul<F>(p.ZZZ, PPP);
   return r;

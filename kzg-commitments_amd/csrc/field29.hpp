@@ -235,6 +235,42 @@ KZGX_DEV F29<F> f29_neg_lazy(const F29<F>& a) {
   return r;
 }
 
+// a + 2 b limb-wise, no carry: for normalized a, b the limbs are < 3 2^29.
+// Only for a f29_sub subtrahend (its int32 carries absorb limbs < 2^31).
+template <class F>
+KZGX_DEV F29<F> f29_add_2x_lazy(const F29<F>& a, const F29<F>& b) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = a.v[i] + 2u * b.v[i];
+  return r;
+}
+
+// 8m - a for normalized a < 4m, no carry chain: one v_sub per limb (P8B's
+// limbs dominate a's limb-wise, see gen_consts.py), result < 8m with limbs
+// in [0, 2^30).  For a product operand whose partner has normalized limbs
+// (f29_mul2's column bound holds with one such operand).
+template <class F>
+KZGX_DEV F29<F> f29_neg8_lazy(const F29<F>& a) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = F::P8B[i] - a.v[i];
+  return r;
+}
+
+// carry-normalize limbs (< 2^31 each) without changing the value
+template <class F>
+KZGX_DEV F29<F> f29_normalize(const F29<F>& a) {
+  F29<F> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const uint32_t s = a.v[i] + c;
+    r.v[i] = i + 1 < F::L ? (s & M29) : s;
+    c = s >> 29;
+  }
+  return r;
+}
+
 // a - K if a >= K (K a multiple of m)
 template <class F>
 KZGX_DEV F29<F> f29_csub(const F29<F>& a, const uint32_t (&K)[F::L]) {

@@ -73,8 +73,16 @@ def field29(name, m, L):
     t = limbs29(2 * m, L)
     b = [t[0] + (1 << 29)] + [t[i] + (1 << 29) - 1 for i in range(1, L - 1)] + [t[L - 1] - 1]
     assert sum(v << (29 * i) for i, v in enumerate(b)) == 2 * m and all(v < (1 << 30) for v in b)
-    assert b[L - 1] >= (m >> (29 * (L - 1))) and all(v >= (1 << 29) - 1 for v in b[:L - 1])
+    assert b[L - 1] >= (m - 1) >> (29 * (L - 1)) and all(v >= (1 << 29) - 1 for v in b[:L - 1])
     lines.append("  static constexpr uint32_t P2B[L] = {%s};  // 2m, limbs borrowed into [2^29-1, 2^30)" %
+                 ", ".join("0x%08xu" % v for v in b))
+    t = limbs29(8 * m, L)
+    b = [t[0] + (1 << 29)] + [t[i] + (1 << 29) - 1 for i in range(1, L - 1)] + [t[L - 1] - 1]
+    assert sum(v << (29 * i) for i, v in enumerate(b)) == 8 * m and all(v < (1 << 30) for v in b)
+    # limb-wise >= every normalized a < 4m: middle limbs >= 2^29 - 1, top limb
+    # >= the top limb of 4m - 1 >= a's top limb
+    assert b[L - 1] >= (4 * m - 1) >> (29 * (L - 1)) and all(v >= (1 << 29) - 1 for v in b[:L - 1])
+    lines.append("  static constexpr uint32_t P8B[L] = {%s};  // 8m, limbs borrowed into [2^29-1, 2^30)" %
                  ", ".join("0x%08xu" % v for v in b))
     lines += [
         "  static constexpr uint32_t R2[L] = %s;  // R^2 mod m" % arr29(R * R % m, L),
