@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--fixed-bits", type=int, default=-1,
                     help="fixed-base table window (0 = Pippenger only; default 16: BN254 171.8 GB, "
                          "BLS12-381 240.6 GB of the 288 GiB HBM)")
-    ap.add_argument("--fixed-ppt", type=int, default=16, help="SRS points per accumulation thread (fixed-base path)")
+    ap.add_argument("--fixed-ppt", type=int, default=16,
+                    help="SRS points per accumulation thread (fixed-base path; 0 = automatic)")
+    ap.add_argument("--table-gb", type=float, default=200.0, help="cfg5: fixed-base table budget per GPU (GB)")
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
     ap.add_argument("--split", type=int, default=1, help="sub-batches (each on its own stream) per batch")
@@ -315,14 +317,16 @@ def main():
                 with open(vpath) as f:
                     vj = json.load(f)
                 # VALU issue roofline of the accumulation kernel: PMC instruction
-                # count per MSM x MSMs per launch / live launch time, against
-                # 1024 SIMDs x 2.4 GHz / (measured mix cost per instruction)
+                # count per launch x launches per step / measured step time (the
+                # two streams' launches overlap, so per-launch event time would
+                # double-count), against 1024 SIMDs x 2.4 GHz / (measured mix
+                # cost per instruction)
                 ipl = vj["valu_insts_per_launch"] * B / vj["batch"]  # one launch = B MSMs of ~4097 points
-                rate = ipl / (avg_launch_ms * 1e-3)
+                rate = ipl * launches_per_step / (elapsed / args.steps)
                 peak = 256 * 4 * 2.4e9 / vj["mix_cost_cycles_per_inst"]
                 valu = {"wave_insts_per_s": rate, "peak_wave_insts_per_s": peak, "frac": rate / peak,
                         "insts_per_wave_mixed_add": vj["valu_insts_per_wave_mixed_add"],
-                        "source": "profiles/pmc_valu_cfg2.json (PMC SQ_INSTS_VALU) + live launch time"}
+                        "source": "profiles/pmc_valu_cfg2.json (PMC SQ_INSTS_VALU) x launches / live step time"}
             except (OSError, ValueError, KeyError):
                 valu = None
         total_units = units_per_step * args.steps * world
@@ -404,6 +408,21 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, max(count, 1), start)
+    # fixed-base table over this rank's shard: the widest window whose table
+    # fits the budget (2^20 points on 1 GPU: c = 7, 198.6 GB; 2^17 per GPU on
+    # 8 GPUs: c = 10, 139.6 GB).  Setup work, outside the timed region.
+    t_setup = time.perf_counter()
+    fixed_bits = args.fixed_bits
+    if fixed_bits < 0:
+        fixed_bits = 0
+        for c in range(16, 6, -1):
+            w = (C.r.bit_length() + 1 + c - 1) // c
+            if w * max(count, 1) * (1 << (c - 1)) * 80 <= args.table_gb * 1e9:
+                fixed_bits = c
+                break
+    if fixed_bits:
+        ctx.set_fixed_base(fixed_bits, max(count, 1))
+    t_setup = time.perf_counter() - t_setup
     rng = np.random.default_rng(0x4B5A47)  # same full polynomial on every rank
     coeffs_h = random_fr(rng, (n,), C.r)
     d_c = torch.from_numpy(coeffs_h[start:start + count].copy().view(np.int64)).to(dev)
@@ -458,8 +477,12 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
             "dtype": "uint32 limbs (254-bit Montgomery Fp)",
             "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 from fixed tau",
             "config": {"workload": "BN254 degree-2^20 commit, point range sharded, all-gather + fold",
-                       "n_coeffs": n, "window_bits": args.window_bits, "segment": args.segment,
+                       "n_coeffs": n, "shard_points": count,
+                       "msm": ("fixed-base table over the shard, c=%d, %.1f GB" % (
+                           fixed_bits, ctx.fixed_base_info()[2] / 1e9)) if fixed_bits else
+                              ("pippenger, c=%d, segment %d" % (args.window_bits, args.segment)),
                        "parallelism": "msm-shard%d" % world},
+            "secondary": {"fixed_table_setup_s": t_setup},
             "parity": {"checked": 1, "ok": int(ok), "method": "[P(tau)]G1 identity"},
         }
         print(json.dumps(line), flush=True)

@@ -87,12 +87,15 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
  * (2 x 32 B BN254, 2 x 48 B BLS12-381).  Every MSM with n <= n_points then
  * runs as a plain sum of table points (no bucket sort / reduction).  Built
  * now if an SRS is installed, else when one is; rebuilt on every SRS change.
- * c = 0 turns it off (Pippenger for every MSM).  c in {4, 8, 10, 12..17};
- * BN254 c = 15 over 4097 points takes 73 GB of device memory. */
+ * c = 0 turns it off (Pippenger for every MSM).  c in {4, 7..17};
+ * BN254 c = 16 over 4097 points takes 171.8 GB of device memory (80-B
+ * radix-2^29 entries). */
 int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
 /* built table: window bits (0 = none), points covered, device bytes */
 int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
-/* SRS points summed per accumulation thread on the fixed-base path (default 16) */
+/* SRS points summed per accumulation thread on the fixed-base path
+ * (0 = automatic, the default: 16 for batches of >= 64 MSMs, else enough
+ * threads to fill the GPU, with a wavefront-level fold for single MSMs) */
 int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p);
 
 /* ---- SRS ---------------------------------------------------------------- */

@@ -235,7 +235,7 @@ int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* 
 
 int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p) {
   KZGX_TRY(activate(ctx));
-  if (p < 1 || p > 1024) return KZGX_ERR_ARG;
+  if (p > 1024) return KZGX_ERR_ARG;  // 0 = automatic
   ctx->c.fixed.pts_per_thread = p;
   return KZGX_OK;
 }

@@ -53,7 +53,7 @@ constexpr int KZGX_MAX_STREAMS = 8;
 struct FixedTable {
   int c_req = 0;        // requested window bits (0 = off)
   size_t n_req = 0;     // requested SRS prefix length
-  uint32_t pts_per_thread = 16;
+  uint32_t pts_per_thread = 0;  // 0 = automatic (fixed_msm_impl)
   int c = 0, W = 0;     // built table
   size_t n_t = 0;
   uint32_t* d = nullptr;
@@ -140,6 +140,8 @@ bool fixed_usable(const Ctx* ctx, size_t n);
 int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out);
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
+// one workgroup sums count XYZZ points -> canonical affine (msm.hip)
+int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st);
 int gen_srs_points(Ctx* ctx, const uint32_t* tau_canon_host, size_t start, size_t n, uint32_t* d_out_canon,

@@ -536,6 +536,17 @@ static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uin
   return KZGX_OK;
 }
 
+int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_xyzz_sum<BN254G1>, dim3(1), dim3(256), 256 * xyzz_words<BN254G1>() * 4, st, d_parts,
+                       (uint32_t)count, d_out, d_out_inf);
+  else
+    hipLaunchKernelGGL(k_xyzz_sum<BLS12381G1>, dim3(1), dim3(256), 256 * xyzz_words<BLS12381G1>() * 4, st, d_parts,
+                       (uint32_t)count, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;

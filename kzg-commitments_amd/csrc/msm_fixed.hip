@@ -25,6 +25,8 @@
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "curve.hpp"
 #include "kzgx_internal.hpp"
 
@@ -424,17 +426,39 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
                           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
   FixedTable& ft = ctx->fixed;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
-  const uint32_t P0 = ft.pts_per_thread;
-  const uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
+  // points per thread: 16 for batches (one MSM ~ 5 wavefronts at degree
+  // 4096, T = 320 partials); for a few large MSMs, enough threads to fill
+  // the 256 CUs x 4 SIMDs x 3 waves of resident slots
+  constexpr size_t kSlots = 256 * 4 * 3 * 64;
+  uint32_t P0 = ft.pts_per_thread;
+  if (P0 == 0) P0 = batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
+  uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
+  // few large MSMs: two wavefront folds (64:1 each) and one workgroup sum
+  // instead of one wavefront per MSM summing T partials; T is padded to a
+  // multiple of 64^2 (the extra threads own no points: identity partials)
+  const bool wave_red = batch <= 16 && T > 1024 && !xyzz_out;
+  if (wave_red) T = (T + 4095) / 4096 * 4096;
   MsmWs* wsp = ctx->ws_for(st);
   if (!wsp) return KZGX_ERR_ARG;
   MsmWs& ws = *wsp;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * T * XB, &ws.fpart_b));
-  KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * XB, &ws.fsum_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * (wave_red ? T / 64 : 1) * XB, &ws.fsum_b));
   {
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
                        (uint32_t)n, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, T, ws.fpart);
+  }
+  if (wave_red) {
+    ProfScope p(ctx, st, "msm_reduce");
+    const size_t g1 = batch * (T / 64), g2 = batch * (T / 4096);
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g1 + 3) / 4)), dim3(256), 0, st, ws.fpart, 64u,
+                       (uint32_t)g1, ws.fsum);
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g2 + 3) / 4)), dim3(256), 0, st, ws.fsum, 64u,
+                       (uint32_t)g2, ws.fpart);
+    const size_t xw = xyzz_words<C>(), pw = 2 * C::Fp::N;
+    for (size_t b = 0; b < batch; b++)
+      KZGX_TRY(xyzz_sum(ctx, ws.fpart + b * (T / 4096) * xw, T / 4096, d_out + b * pw, d_out_inf + b, st));
+    return KZGX_OK;
   }
   {
     ProfScope p(ctx, st, "msm_reduce");
@@ -454,8 +478,11 @@ static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t bat
 #define KZGX_FIXED_CASE(cb) \
   case cb: return fixed_msm_impl<C, cb>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
     KZGX_FIXED_CASE(4)
+    KZGX_FIXED_CASE(7)
     KZGX_FIXED_CASE(8)
+    KZGX_FIXED_CASE(9)
     KZGX_FIXED_CASE(10)
+    KZGX_FIXED_CASE(11)
     KZGX_FIXED_CASE(12)
     KZGX_FIXED_CASE(13)
     KZGX_FIXED_CASE(14)
@@ -468,7 +495,7 @@ static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t bat
 }
 
 bool fixed_bits_supported(int c) {
-  return c == 0 || c == 4 || c == 8 || c == 10 || (c >= 12 && c <= 17);
+  return c == 0 || c == 4 || (c >= 7 && c <= 17);
 }
 
 bool fixed_usable(const Ctx* ctx, size_t n) { return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t; }

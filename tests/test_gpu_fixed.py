@@ -144,7 +144,7 @@ def test_fixed_coverage_and_fallback(fresh_ctx, oracle_c):
     out, inf = ctx.msm(S[:200])
     assert pt(name, out, inf) == K.commit_via_tau(C, tau + 1, sc[:200])
     with pytest.raises(Exception):
-        ctx.set_fixed_base(7, 100)  # unsupported window
+        ctx.set_fixed_base(5, 100)  # unsupported window
     with pytest.raises(Exception):
         ctx.set_fixed_base(8, 0)
 
@@ -170,3 +170,23 @@ def test_fixed_degree4096_batch(name, C, c, fresh_ctx):
     for j, z in enumerate(zs):
         q = K.proof_quotient(C, polys[0], z, 1)
         assert pt(name, pout[j], pinf[j]) == K.commit_via_tau(C, tau, q), z
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("batch", [1, 3])
+def test_fixed_large_single_msm(name, C, batch, fresh_ctx):
+    """few large MSMs on the fixed-base path (configs[4] shape, scaled down):
+    automatic points-per-thread fills the GPU, each wavefront folds its 64
+    partials, one workgroup sums the rest; identity commit == [P(tau)]G1"""
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C)
+    n = 70001
+    ctx.gen_srs(tau, n)
+    ctx.set_fixed_base(7, n)
+    polys = [K.random_scalars(C, n, seed=900 + b) for b in range(batch)]
+    polys[0][5] = 0
+    S = np.concatenate([limbs(P) for P in polys])
+    out, inf = ctx.msm_batch(S, n, batch)
+    for b in range(batch):
+        exp = K.commit_via_tau(C, tau, polys[b])
+        assert pt(name, out[b], inf[b]) == exp
