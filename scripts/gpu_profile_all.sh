@@ -3,6 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out/prof gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
 cut -c1-300 gpurun_out/bench_default.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || { echo "prof failed"; tail -20 gpurun_out/prof_bench.err; exit 1; }
