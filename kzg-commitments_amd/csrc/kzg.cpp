@@ -600,6 +600,11 @@ std::vector<G1> trusted_setup::g1_points() const {
   return res;
 }
 
+void trusted_setup::precompute(int window_bits, size_t points) {
+  check(kzgx_set_fixed_base(ctx, window_bits, window_bits ? (points ? std::min(points, n) : n) : 0),
+        "kzgx_set_fixed_base");
+}
+
 std::vector<G2> trusted_setup::g2_points() const {
   const int nl = base_limbs();
   const size_t n2 = kzgx_srs_g2_size(ctx);

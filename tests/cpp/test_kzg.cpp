@@ -206,6 +206,15 @@ int main(int argc, char** argv) {
       agree = kzg.verify_proof(vc[t], vpf[t], b) == vr[t];
     }
     check_test(agree, "verify_proofs == verify_proof (3 valid, 1 refuted)");
+    // fixed-base table: the same commitments and proofs as the table-less MSM
+    kzg.precompute(8, 0);
+    auto cs2 = kzg.create_commits(ps);
+    auto prs2 = kzg.create_proofs(ps[4], {0, 3, 184});
+    same = true;
+    for (int i = 0; i < 5; i++) same &= cs2[i].get_curve_point() == cs[i].get_curve_point();
+    for (int t = 0; t < 3; t++) same &= prs2[t].get_curve_point() == prs[t].get_curve_point();
+    check_test(same, "precompute(8): fixed-base table results == Pippenger results");
+    kzg.precompute(0);
   }
 
   // bad octets deserialize to infinity (util.cpp:107-112)
