@@ -92,6 +92,38 @@ def random_fr(rng, shape, r):
         w[ge] = fresh
 
 
+def fixed_table_bytes(curve, c, npts):
+    """device bytes of the fixed-base table (msm_fixed.hip: W x n x 2^(c-1)
+    entries of 80 B (BN254) / 112 B (BLS12-381) radix-2^29 affine points)"""
+    bits = 254 if curve == "BN254" else 255
+    w = (bits + 1 + c - 1) // c
+    return w * npts * (1 << (c - 1)) * (80 if curve == "BN254" else 112)
+
+
+def set_fixed_with_fallback(kzgx, ctx, c, npts, budget=None):
+    """build the fixed-base table at the widest window <= c that fits the
+    device's free memory (minus 8 GB for workspaces) and the optional budget;
+    a failed allocation steps the window down once more.  Returns the window
+    built (0 = none: Pippenger)."""
+    import torch
+    free = torch.cuda.mem_get_info()[0] - 8e9
+    if budget is not None:
+        free = min(free, budget)
+    while c >= 7 and fixed_table_bytes(ctx.curve, c, npts) > free:
+        c -= 1
+    while c >= 7:
+        try:
+            ctx.set_fixed_base(c, npts)
+            return c
+        except kzgx.KzgxError as e:
+            if e.status != -3:  # KZGX_ERR_OOM
+                raise
+            print("bench: fixed-base table c=%d did not fit, trying c=%d" % (c, c - 1), file=sys.stderr)
+            c -= 1
+    ctx.set_fixed_base(0, 0)
+    return 0
+
+
 def to_int(row):
     return sum(int(row[i]) << (64 * i) for i in range(len(row)))
 
@@ -129,7 +161,7 @@ def main():
     if fixed_bits:
         # precompute the signed-digit multiples of the 4097-point SRS prefix
         # (setup time, like the reference's trusted_setup ctor; not timed)
-        ctx.set_fixed_base(fixed_bits, n)
+        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, n)
         ctx.set_fixed_points_per_thread(args.fixed_ppt)
     t_setup = time.perf_counter() - t_setup
     fb = ctx.fixed_base_info()
@@ -412,16 +444,9 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     # fits the budget (2^20 points on 1 GPU: c = 7, 198.6 GB; 2^17 per GPU on
     # 8 GPUs: c = 10, 139.6 GB).  Setup work, outside the timed region.
     t_setup = time.perf_counter()
-    fixed_bits = args.fixed_bits
-    if fixed_bits < 0:
-        fixed_bits = 0
-        for c in range(16, 6, -1):
-            w = (C.r.bit_length() + 1 + c - 1) // c
-            if w * max(count, 1) * (1 << (c - 1)) * 80 <= args.table_gb * 1e9:
-                fixed_bits = c
-                break
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
     if fixed_bits:
-        ctx.set_fixed_base(fixed_bits, max(count, 1))
+        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1), budget=args.table_gb * 1e9)
     t_setup = time.perf_counter() - t_setup
     rng = np.random.default_rng(0x4B5A47)  # same full polynomial on every rank
     coeffs_h = random_fr(rng, (n,), C.r)
