@@ -180,13 +180,15 @@ int kzgx_pairing(kzgx_ctx* ctx, const uint64_t* g1_xy, const int* g1_inf, const 
 /* trusted_setup::verify_proof (src/trusted_setup.cpp:230-254): *ok =
  * e(proof, [Z(tau)]G2) == e(C - [I(tau)]G1, G2[0]) for the npoints opened
  * points (xs, ys); npoints >= |SRS G1| gives *ok = 0; npoints == 0 is
- * KZGX_ERR_ARG; needs a G2 setup of >= npoints + 1 points. */
+ * KZGX_ERR_ARG; needs a G2 setup of >= npoints + 1 points.  npoints == 1
+ * runs as kzgx_verify_single_batch with one opening (same boolean). */
 int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, const uint64_t* proof_xy,
                       int proof_inf, const uint64_t* xs, const uint64_t* ys, size_t npoints, int* ok);
 /* batch of single-point verifies (verify_proof with one opened point each):
  * ok[k] = e(proof_k, [tau - z_k]G2) == e(commit_k - [y_k]G1, G2), evaluated as
- * one two-Miller-loop product and one final exponentiation per opening, one
- * GPU thread each.  Needs G1[0] = G and G2[0..1]; inf arrays may be NULL. */
+ * one two-Miller-loop product and one final exponentiation per opening (a
+ * wave or a lane each, see kzgx_set_verify_wave_max).  Needs G1[0] = G and
+ * G2[0..1]; inf arrays may be NULL. */
 int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const int* commit_inf,
                              const uint64_t* proofs_xy, const int* proof_inf, const uint64_t* zs, const uint64_t* ys,
                              size_t count, int* ok);
@@ -194,6 +196,11 @@ int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const in
 int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const void* d_commit_inf,
                                     const void* d_proofs, const void* d_proof_inf, const void* d_z, const void* d_y,
                                     size_t count, void* d_ok, void* stream);
+/* Batches of at most max_count openings (default 4096) run one 64-lane wave
+ * per opening (Fp12 products spread over the wave, setup-derived line and
+ * [y]G tables built on first use); larger batches run one lane per opening.
+ * Both give the same booleans; 0 forces the lane-per-opening kernel. */
+int kzgx_set_verify_wave_max(kzgx_ctx* ctx, size_t max_count);
 
 #ifdef __cplusplus
 }

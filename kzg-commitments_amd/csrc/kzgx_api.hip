@@ -21,6 +21,12 @@ struct kzgx_ctx {
   uint32_t* d_srs2_canon = nullptr;  // installed G2 SRS, canonical affine (x.re, x.im, y.re, y.im)
   size_t srs2_canon_b = 0;
   size_t n_srs2 = 0;
+  // wave-per-opening verify: tables derived from G1[0], G2[0..1] (built on
+  // first use, dropped when either SRS changes)
+  uint32_t* d_vw = nullptr;
+  size_t vw_b = 0;
+  bool vw_ready = false;
+  size_t vw_max = 8192;  // batches up to this size take the wave path
 };
 
 namespace kzgx {
@@ -133,7 +139,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
-                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws};
+                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   kzgx::fixed_free(&c);
@@ -246,6 +252,7 @@ size_t kzgx_srs_size(const kzgx_ctx* ctx) { return ctx ? ctx->c.n_srs : 0; }
 
 int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
   KZGX_TRY(activate(ctx));
+  ctx->vw_ready = false;
   if (!xy || n == 0) return KZGX_ERR_ARG;
   const size_t bytes = n * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs_canon, bytes, &ctx->srs_canon_b));
@@ -257,6 +264,7 @@ int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
 
 int kzgx_gen_srs_g1(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
   KZGX_TRY(activate(ctx));
+  ctx->vw_ready = false;
   if (!tau || n == 0 || n > 0x7fffffffu) return KZGX_ERR_ARG;
   const size_t bytes = n * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs_canon, bytes, &ctx->srs_canon_b));
@@ -516,6 +524,7 @@ size_t kzgx_srs_g2_size(const kzgx_ctx* ctx) { return ctx ? ctx->n_srs2 : 0; }
 
 int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
   KZGX_TRY(activate(ctx));
+  ctx->vw_ready = false;
   if (!tau || n == 0 || n > 0x7fffffffu) return KZGX_ERR_ARG;
   const size_t bytes = n * 2 * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
@@ -530,6 +539,7 @@ int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) 
 
 int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
   KZGX_TRY(activate(ctx));
+  ctx->vw_ready = false;
   if (!xy || n == 0) return KZGX_ERR_ARG;
   const size_t bytes = n * 2 * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
@@ -622,6 +632,10 @@ int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, 
   *ok = 0;
   if (npoints >= ctx->c.n_srs) return KZGX_OK;  // trusted_setup.cpp:235-236
   if (ctx->n_srs2 < npoints + 1) return KZGX_ERR_NO_SRS;
+  if (npoints == 1) {  // I = y, Z = X - x: the single-opening product check
+    const int cf = commit_inf != 0, pf = proof_inf != 0;
+    return kzgx_verify_single_batch(ctx, commit_xy, &cf, proof_xy, &pf, xs, ys, 1, ok);
+  }
   hipStream_t st = ctx->c.stream;
   const size_t n = npoints;
   const size_t p1 = point_words(ctx) * 4, p2 = 2 * p1, fb = 6 * p1;
@@ -668,10 +682,27 @@ int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const 
   if (count == 0) return KZGX_OK;
   if (!d_commits || !d_proofs || !d_z || !d_y || !d_ok || count > (1u << 26)) return KZGX_ERR_ARG;
   if (ctx->c.n_srs == 0 || ctx->n_srs2 < 2) return KZGX_ERR_NO_SRS;
+  hipStream_t st = pick(ctx, stream);
+  if (count <= ctx->vw_max) {
+    if (!ctx->vw_ready) {
+      KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
+      KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, ctx->d_vw, st));
+      ctx->vw_ready = true;
+    }
+    return kzgx::verify_wave_batch(&ctx->c, (const uint32_t*)d_commits, (const uint32_t*)d_commit_inf,
+                                   (const uint32_t*)d_proofs, (const uint32_t*)d_proof_inf, (const uint32_t*)d_z,
+                                   (const uint32_t*)d_y, count, ctx->d_srs_canon, ctx->d_vw, (uint32_t*)d_ok, st);
+  }
   return kzgx::verify_single_batch(&ctx->c, (const uint32_t*)d_commits, (const uint32_t*)d_commit_inf,
                                    (const uint32_t*)d_proofs, (const uint32_t*)d_proof_inf, (const uint32_t*)d_z,
                                    (const uint32_t*)d_y, count, ctx->d_srs_canon, ctx->d_srs2_canon,
-                                   (uint32_t*)d_ok, pick(ctx, stream));
+                                   (uint32_t*)d_ok, st);
+}
+
+int kzgx_set_verify_wave_max(kzgx_ctx* ctx, size_t max_count) {
+  if (!ctx) return KZGX_ERR_ARG;
+  ctx->vw_max = max_count;
+  return KZGX_OK;
 }
 
 int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const int* commit_inf,

@@ -171,6 +171,12 @@ int pairing_batch(Ctx* ctx, const uint32_t* d_g1, const uint32_t* d_g1_inf, cons
 int verify_single_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
                         const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
                         const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_ok, hipStream_t st);
+// wave-per-opening verify (pairing.hip): setup-derived tables, then the batch
+size_t verify_wave_bytes(int curve);
+int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st);
+int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
+                      const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
+                      const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st);
 int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 

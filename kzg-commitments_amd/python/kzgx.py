@@ -28,7 +28,7 @@ EXPORTS = [
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
-    "kzgx_verify_single_batch_device",
+    "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max",
 ]
 
 _lib = None
@@ -92,6 +92,7 @@ def lib():
             "kzgx_verify_proof": (ctypes.c_int, [vp, u64p, ctypes.c_int, u64p, ctypes.c_int, u64p, u64p, sz, intp]),
             "kzgx_verify_single_batch": (ctypes.c_int, [vp, u64p, intp, u64p, intp, u64p, u64p, sz, intp]),
             "kzgx_verify_single_batch_device": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, sz, vp, vp]),
+            "kzgx_set_verify_wave_max": (ctypes.c_int, [vp, sz]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -356,6 +357,10 @@ class Context:
                                             None if fp is None else fp.ctypes.data_as(intp), _p(z), _p(y), n,
                                             ok.ctypes.data_as(intp)), "kzgx_verify_single_batch")
         return ok.astype(bool)
+
+    def set_verify_wave_max(self, max_count: int) -> None:
+        """batches of <= max_count openings run a wave per opening (0: a lane each)"""
+        _chk(lib().kzgx_set_verify_wave_max(self.h, max_count), "kzgx_set_verify_wave_max")
 
     def verify_single_batch_device(self, d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y, count, d_ok,
                                    stream=None):

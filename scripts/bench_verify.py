@@ -81,6 +81,24 @@ def main():
     res["single_verifies"] = nv
     res["single_verifies_per_s"] = nv / dt
     res["single_verifies_all_ok"] = bool(ok.all())
+    # wave-per-opening vs lane-per-opening kernels over batch sizes
+    sweep = {}
+    for m in (1, 16, 256, 1024, 4096, 16384):
+        if m > nv:
+            break
+        row = {}
+        for mode, wmax in (("wave", 1 << 30), ("lane", 0)):
+            ctx.set_verify_wave_max(wmax)
+            ok = ctx.verify_single_batch(cc[:m], prf[:m], zs[:m], yv[:m])  # warm-up (+ tables)
+            reps = 5 if m <= 256 else 2
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ok = ctx.verify_single_batch(cc[:m], prf[:m], zs[:m], yv[:m])
+            dt = (time.perf_counter() - t0) / reps
+            row[mode] = {"ms": dt * 1e3, "per_s": m / dt, "all_ok": bool(ok.all())}
+        sweep[str(m)] = row
+    ctx.set_verify_wave_max(8192)
+    res["single_verify_sweep"] = sweep
     res["reference_readme_ms"] = {"verify_1": 3.109, "verify_2048": 1599.394, "source": "README.md:130-144 (BN254)"}
     print(json.dumps(res), flush=True)
     ctx.close()

@@ -227,11 +227,14 @@ def test_verify_proof_degenerate_setups(name, C, ctxs):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-def test_verify_single_batch(name, C, ctxs):
+@pytest.mark.parametrize("wave_max", [4096, 0], ids=["wave", "lane"])
+def test_verify_single_batch(name, C, ctxs, wave_max):
     """batched single-point verifies == verify_proof(commit, proof, {(z, y)})
     (reference trusted_setup.cpp:230-254 with one point), against the
-    known-tau oracle on valid and tampered openings"""
+    known-tau oracle on valid and tampered openings; both kernels (a wave per
+    opening, a lane per opening)"""
     ctx = ctxs(name)
+    ctx.set_verify_wave_max(wave_max)
     tau = K.default_tau(C)
     _setup(ctx, C, tau, 64)
     polys = [K.random_scalars(C, 40, seed=100 + i) for i in range(3)] + [[0] * 40]
@@ -264,3 +267,4 @@ def test_verify_single_batch(name, C, ctxs):
                                   proof_inf=pis)
     assert got.tolist() == exp
     assert sum(exp) >= 16  # the valid openings (and the zero polynomial's degenerate ones)
+    ctx.set_verify_wave_max(8192)
