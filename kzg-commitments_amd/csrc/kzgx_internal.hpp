@@ -177,6 +177,12 @@ int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_0
 int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
                       const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
                       const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st);
+// one wave: *ok = e(P_0, Q_0) e(-P_1, Q_1) == 1 (p: 2 canonical affine G1
+// points, q: 2 canonical G2 points, inf flags may be NULL; scratch of
+// pair2_wave_scratch_bytes for the line tables)
+size_t pair2_wave_scratch_bytes(int curve);
+int pair2_wave(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+               uint32_t* d_scratch, uint32_t* d_ok, hipStream_t st);
 int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 

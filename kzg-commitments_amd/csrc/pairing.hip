@@ -964,6 +964,56 @@ KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
   if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C>(f, f);
 }
 
+// the product of the two pairings (P_q, Q_q), q = 0, 1, from the line tables
+// of Q_0, Q_1 (k_vlines) and the per-pairing scale factors and use flags the
+// caller left in LDS (scale: [q][yP, xP, 1] up to an Fp factor; flag[q]);
+// *ok_out = (product after the final exponentiation == 1)
+template <class C>
+KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __restrict__ ok_out) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int L = V::L, E2 = V::E2;
+  uint32_t* lines = vw_smem + V::O_LINES;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  const int lane = threadIdx.x;
+  const bool use0 = flag[0] != 0, use1 = flag[1] != 0;
+  // ---- scale the precomputed lines
+  for (int t = lane; t < 2 * V::NL * 3; t += 64) {
+    const int q = t / (3 * V::NL), c = t % 3;
+    const uint32_t* src = vlines + (size_t)t * E2;  // [q][s][c] order matches t
+    vw_st2<C>(lines + t * E2, f2_mul_fp<C>(vw_ld2<C>(src), vw_ld<C>(scale + (q * 3 + c) * L)));
+  }
+  // f = 1
+  constexpr uint32_t f = V::O_SLOT, pr = V::O_PROD;
+  if (lane < 12) vw_st<C>(vw_smem + f + lane * L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  __syncthreads();
+  VW_STAMP(3);
+  vw_miller<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr);
+  VW_STAMP(4);
+  vw_final_exp<C>(V::O_SLOT, pr);
+  VW_STAMP(8);
+  // ---- f == 1 ?
+  if (lane < 12) {
+    const F29<F> v = f29_reduce<F>(vw_ld<C>(vw_smem + f + lane * L));
+    const F29<F> want = lane == 0 ? f29_reduce<F>(f29_one<F>()) : f29_zero<F>();
+    uint32_t diff = 0;
+    for (int i = 0; i < L; i++) diff |= v.v[i] ^ want.v[i];
+    flag[2 + lane] = diff;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t bad = 0;
+    for (int i = 0; i < 12; i++) bad |= flag[2 + i];
+    *ok_out = bad == 0 ? 1u : 0u;
+#ifdef KZGX_VW_TIMING
+    if (blockIdx.x == 0)
+      printf("vw_ts tree %llu d %llu scale %llu miller %llu final_exp %llu (x10ns)\n", vw_ts[1] - vw_ts[0],
+             vw_ts[2] - vw_ts[1], vw_ts[3] - vw_ts[2], vw_ts[4] - vw_ts[3], vw_ts[8] - vw_ts[4]);
+#endif
+  }
+}
+
 // block (one wave) per opening; same contract as k_verify_single
 template <class C>
 __global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__ commits,
@@ -975,10 +1025,8 @@ __global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ vtab, const uint32_t* __restrict__ vlines,
                                                     const uint32_t* __restrict__ qfin, uint32_t* __restrict__ ok) {
   using F = typename C::Fp29;
-  using P = typename PairOf<C>::T;
   using V = VWave<C>;
-  constexpr int N = C::Fp::N, L = V::L, E2 = V::E2;
-  uint32_t* lines = vw_smem + V::O_LINES;
+  constexpr int N = C::Fp::N, L = V::L;
   uint32_t* prod = vw_smem + V::O_PROD;
   uint32_t* scale = vw_smem + V::O_SCALE;
   uint32_t* flag = vw_smem + V::O_FLAG;
@@ -1035,41 +1083,35 @@ __global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__
   }
   __syncthreads();
   VW_STAMP(2);
-  const bool use0 = flag[0] != 0, use1 = flag[1] != 0;
-  // ---- scale the precomputed lines
-  for (int t = lane; t < 2 * V::NL * 3; t += 64) {
-    const int q = t / (3 * V::NL), c = t % 3;
-    const uint32_t* src = vlines + (size_t)t * E2;  // [q][s][c] order matches t
-    vw_st2<C>(lines + t * E2, f2_mul_fp<C>(vw_ld2<C>(src), vw_ld<C>(scale + (q * 3 + c) * L)));
+  vw_pair_tail<C>(vlines, ok + k);
+}
+
+// one wave: e(P_0, Q_0) e(-P_1, Q_1) == 1 for canonical affine G1 points
+// p = (P_0, P_1) and the line tables of (Q_0, Q_1); the pairing-equation form
+// of verify_proof with more than one point (e(pi, [Z(tau)]G2) ==
+// e(C - [I(tau)]G1, G2[0]))
+template <class C>
+__global__ __launch_bounds__(64) void k_pair2_wave(const uint32_t* __restrict__ p, const uint32_t* __restrict__ p_inf,
+                                                   const uint32_t* __restrict__ q_inf,
+                                                   const uint32_t* __restrict__ vlines,
+                                                   const uint32_t* __restrict__ qfin, uint32_t* __restrict__ ok) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int N = C::Fp::N, L = V::L;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 2; q++) {
+      Affine<C> a;
+      const bool fin = affine_from_canonical<C>(p + q * 2 * N, a) && !(p_inf && p_inf[q]);
+      vw_st<C>(scale + (q * 3 + 0) * L, q ? fp_neg<F>(a.y) : a.y);
+      vw_st<C>(scale + (q * 3 + 1) * L, a.x);
+      vw_st<C>(scale + (q * 3 + 2) * L, f29_one<F>());
+      flag[q] = (fin && qfin[q] && !(q_inf && q_inf[q])) ? 1u : 0u;
+    }
   }
-  // f = 1
-  constexpr uint32_t f = V::O_SLOT, pr = V::O_PROD;
-  if (lane < 12) vw_st<C>(vw_smem + f + lane * L, lane == 0 ? f29_one<F>() : f29_zero<F>());
   __syncthreads();
-  VW_STAMP(3);
-  vw_miller<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr);
-  VW_STAMP(4);
-  vw_final_exp<C>(V::O_SLOT, pr);
-  VW_STAMP(8);
-  // ---- f == 1 ?
-  if (lane < 12) {
-    const F29<F> v = f29_reduce<F>(vw_ld<C>(vw_smem + f + lane * L));
-    const F29<F> want = lane == 0 ? f29_reduce<F>(f29_one<F>()) : f29_zero<F>();
-    uint32_t diff = 0;
-    for (int i = 0; i < L; i++) diff |= v.v[i] ^ want.v[i];
-    flag[2 + lane] = diff;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    uint32_t bad = 0;
-    for (int i = 0; i < 12; i++) bad |= flag[2 + i];
-    ok[k] = bad == 0 ? 1u : 0u;
-#ifdef KZGX_VW_TIMING
-    if (k == 0)
-      printf("vw_ts tree %llu d %llu scale %llu miller %llu final_exp %llu (x10ns)\n", vw_ts[1] - vw_ts[0],
-             vw_ts[2] - vw_ts[1], vw_ts[3] - vw_ts[2], vw_ts[4] - vw_ts[3], vw_ts[8] - vw_ts[4]);
-#endif
-  }
+  vw_pair_tail<C>(vlines, ok);
 }
 
 // ---- host side ----------------------------------------------------------------
@@ -1209,6 +1251,29 @@ int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_com
                                          d_buf, d_ok, st)
              : verify_wave_impl<BLS12381G1>(d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y, count, d_g1_0,
                                             d_buf, d_ok, st);
+}
+
+template <class C>
+static int pair2_wave_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+                           uint32_t* d_lines, uint32_t* d_ok, hipStream_t st) {
+  uint32_t* qfin = d_lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
+  hipLaunchKernelGGL(k_vlines<C>, dim3(1), dim3(64), 0, st, d_q, d_lines, qfin);
+  hipLaunchKernelGGL(k_pair2_wave<C>, dim3(1), dim3(64), VWave<C>::WORDS * 4, st, d_p, d_p_inf, d_q_inf, d_lines,
+                     qfin, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+size_t pair2_wave_scratch_bytes(int curve) {
+  return 4 * (curve == KZGX_CURVE_BN254 ? (size_t)2 * VWave<BN254G1>::NL * VWave<BN254G1>::LW + 4
+                                        : (size_t)2 * VWave<BLS12381G1>::NL * VWave<BLS12381G1>::LW + 4);
+}
+
+int pair2_wave(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+               uint32_t* d_scratch, uint32_t* d_ok, hipStream_t st) {
+  ProfScope p(ctx, st, "pair2_wave");
+  return ctx->curve == KZGX_CURVE_BN254 ? pair2_wave_impl<BN254G1>(d_p, d_p_inf, d_q, d_q_inf, d_scratch, d_ok, st)
+                                        : pair2_wave_impl<BLS12381G1>(d_p, d_p_inf, d_q, d_q_inf, d_scratch, d_ok, st);
 }
 
 int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
