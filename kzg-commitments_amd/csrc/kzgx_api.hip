@@ -27,6 +27,10 @@ struct kzgx_ctx {
   size_t vw_b = 0;
   bool vw_ready = false;
   size_t vw_max = 8192;  // batches up to this size take the wave path
+  // windowed multiples of the G2 SRS for polyeval_G2 (built on first use)
+  uint32_t* d_g2tab = nullptr;
+  size_t g2tab_b = 0;
+  size_t g2tab_n = 0;  // points covered; 0 = stale
 };
 
 namespace kzgx {
@@ -139,7 +143,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
-                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw};
+                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw, ctx->d_g2tab};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   kzgx::fixed_free(&c);
@@ -520,11 +524,28 @@ int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t cou
 }
 
 /* ---- verify half: G2 SRS, polyeval_G2, pairing, verify_proof ---------------- */
+namespace {
+// the G2 SRS's windowed table for n points (rebuilt when the SRS changed or
+// more points are needed); nullptr (plain per-term path) if it cannot be had
+const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
+  if (ctx->g2tab_n >= n) return ctx->d_g2tab;
+  const size_t all = ctx->n_srs2;
+  ctx->g2tab_n = 0;
+  if (kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_g2tab, kzgx::g2_table_bytes(ctx->c.curve, all), &ctx->g2tab_b) !=
+          KZGX_OK ||
+      kzgx::g2_table_build(&ctx->c, ctx->d_srs2_canon, all, ctx->d_g2tab, st) != KZGX_OK)
+    return nullptr;
+  ctx->g2tab_n = all;
+  return ctx->d_g2tab;
+}
+}  // namespace
+
 size_t kzgx_srs_g2_size(const kzgx_ctx* ctx) { return ctx ? ctx->n_srs2 : 0; }
 
 int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
   KZGX_TRY(activate(ctx));
   ctx->vw_ready = false;
+  ctx->g2tab_n = 0;
   if (!tau || n == 0 || n > 0x7fffffffu) return KZGX_ERR_ARG;
   const size_t bytes = n * 2 * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
@@ -540,6 +561,7 @@ int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) 
 int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
   KZGX_TRY(activate(ctx));
   ctx->vw_ready = false;
+  ctx->g2tab_n = 0;
   if (!xy || n == 0) return KZGX_ERR_ARG;
   const size_t bytes = n * 2 * point_words(ctx) * 4;
   KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_srs2_canon, bytes, &ctx->srs2_canon_b));
@@ -588,7 +610,8 @@ int kzgx_msm_g2(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out_
   KZGX_TRY(stage(ctx, 1, pb + 16, &d_o));
   if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, ctx->c.stream));
   uint32_t* d_oi = (uint32_t*)((char*)d_o + pb);
-  KZGX_TRY(kzgx::msm_g2(&ctx->c, (const uint32_t*)d_s, ctx->d_srs2_canon, n, (uint32_t*)d_o, d_oi, ctx->c.stream));
+  KZGX_TRY(kzgx::msm_g2(&ctx->c, (const uint32_t*)d_s, ctx->d_srs2_canon, n, (uint32_t*)d_o, d_oi, ctx->c.stream,
+                        n ? g2_table(ctx, n, ctx->c.stream) : nullptr));
   uint32_t oi = 0;
   KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, pb, hipMemcpyDeviceToHost, ctx->c.stream));
   KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, ctx->c.stream));
@@ -665,7 +688,8 @@ int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, 
                         fl + 5, (uint32_t*)((char*)g1 + p1), fl + 1, st));
   // p1 = [Z(tau)]G2, second pairing's G2 input = G2[0]
   uint32_t* g2 = (uint32_t*)(b + o_g2);
-  KZGX_TRY(kzgx::msm_g2(&ctx->c, (const uint32_t*)(b + o_Z), ctx->d_srs2_canon, n + 1, g2, fl + 2, st));
+  KZGX_TRY(
+      kzgx::msm_g2(&ctx->c, (const uint32_t*)(b + o_Z), ctx->d_srs2_canon, n + 1, g2, fl + 2, st, g2_table(ctx, n + 1, st)));
   KZGX_TRY_HIP(hipMemcpyAsync((char*)g2 + p2, ctx->d_srs2_canon, p2, hipMemcpyDeviceToDevice, st));
   // e(proof, p1) == e(p2, G2[0])  <=>  e(proof, p1) e(-p2, G2[0]) == 1 (one wave, one final
   // exponentiation; the booleans of the reference's FP12_equals)

@@ -163,8 +163,12 @@ int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t 
 
 // verify path: G2 SRS, polyeval_G2, pairing (pairing.hip)
 int gen_srs_g2_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, uint32_t* d_out, hipStream_t st);
+// d_tab (optional): g2_table_build's windowed multiples of the G2 SRS
+size_t g2_table_bytes(int curve, size_t n);
+int g2_table_build(Ctx* ctx, const uint32_t* d_srs2, size_t n, uint32_t* d_tab, hipStream_t st);
 int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
-           uint32_t* d_out_inf, hipStream_t st);
+           uint32_t* d_out_inf, hipStream_t st,
+           const uint32_t* d_tab = nullptr);
 int g2_validate(Ctx* ctx, const uint32_t* d_xy, size_t count, uint32_t* d_ok, hipStream_t st);
 int pairing_batch(Ctx* ctx, const uint32_t* d_g1, const uint32_t* d_g1_inf, const uint32_t* d_g2,
                   const uint32_t* d_g2_inf, size_t count, uint32_t* d_out, hipStream_t st);

@@ -23,6 +23,8 @@
 // single-lane code by design; many pairings (batched verifies) fill waves.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "kzgx_internal.hpp"
 #include "tower.hpp"
 
@@ -294,6 +296,80 @@ __global__ __launch_bounds__(64) void k_g2_sum(const G2J<C>* __restrict__ terms,
   for (uint32_t k = 1; k < 64; k++) acc = g2_add<C>(acc, part[k]);
   G2A<C> a;
   const bool fin = g2_to_affine<C>(acc, a);
+  g2_to_canon<C>(a, fin, out);
+  *out_inf = fin ? 0u : 1u;
+}
+
+// Windowed G2 MSM: tab[i][w] = 2^(16 w) G2[i] (affine Montgomery, zeros for
+// an infinite SRS point), so term i = sum_w d_(i,w) tab[i][w] with 16-bit
+// digits: one thread per (term, window) runs at most 16 doublings and 16
+// additions instead of a 256-bit double-and-add, and the n 16 partial
+// points are folded 8:1 per pass, then by a one-workgroup tree.
+constexpr int G2_TAB_W = 16;
+
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_tab(const uint32_t* __restrict__ srs2, uint32_t n,
+                                               G2A<C>* __restrict__ tab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2A<C> q;
+  const bool fin = g2_from_canon<C>(srs2 + (size_t)i * 4 * C::Fp::N, q);
+  G2J<C> b = g2_from_affine<C>(q);
+  for (int w = 0; w < G2_TAB_W; w++) {
+    G2A<C> a;
+    if (!fin || !g2_to_affine<C>(b, a)) a.x = a.y = f2_zero<C>();
+    tab[(size_t)i * G2_TAB_W + w] = a;
+    if (w + 1 < G2_TAB_W)
+      for (int k = 0; k < 16; k++) b = g2_dbl<C>(b);
+  }
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_terms_w(const uint32_t* __restrict__ scalars,
+                                                   const uint32_t* __restrict__ srs2, const G2A<C>* __restrict__ tab,
+                                                   uint32_t n, G2J<C>* __restrict__ terms) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * G2_TAB_W) return;
+  const uint32_t i = t / G2_TAB_W, w = t % G2_TAB_W;
+  const uint32_t d = (scalars[(size_t)i * 8 + (w >> 1)] >> (16 * (w & 1))) & 0xffffu;
+  G2A<C> q;
+  G2J<C> acc = g2_inf<C>();
+  if (d != 0 && g2_from_canon<C>(srs2 + (size_t)i * 4 * C::Fp::N, q)) {
+    const G2A<C> b = tab[t];
+    for (int k = 31 - __builtin_clz(d); k >= 0; k--) {
+      acc = g2_dbl<C>(acc);
+      if ((d >> k) & 1u) acc = g2_add_mixed<C>(acc, b);
+    }
+  }
+  terms[t] = acc;
+}
+
+// out[t] = sum of in[8 t .. 8 t + 7] (bounded by count)
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_fold8(const G2J<C>* __restrict__ in, uint32_t count,
+                                                 G2J<C>* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t * 8 >= count) return;
+  G2J<C> acc = in[t * 8];
+  for (uint32_t k = t * 8 + 1; k < count && k < t * 8 + 8; k++) acc = g2_add<C>(acc, in[k]);
+  out[t] = acc;
+}
+
+// <= 64 points: one workgroup, LDS tree, lane 0 normalizes
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_sum_tree(const G2J<C>* __restrict__ in, uint32_t count,
+                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  __shared__ G2J<C> part[64];
+  const uint32_t t = threadIdx.x;
+  part[t] = t < count ? in[t] : g2_inf<C>();
+  __syncthreads();
+  for (uint32_t s = 32; s >= 1; s >>= 1) {
+    if (t < s) part[t] = g2_add<C>(part[t], part[t + s]);
+    __syncthreads();
+  }
+  if (t != 0) return;
+  G2A<C> a;
+  const bool fin = g2_to_affine<C>(part[0], a);
   g2_to_canon<C>(a, fin, out);
   *out_inf = fin ? 0u : 1u;
 }
@@ -637,6 +713,24 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
   __syncthreads();
 }
 
+// as lin_fin for positive parts up to 32 units (value < 64m + 32m)
+template <class F>
+KZGX_DEV F29<F> lin_fin_wide(const LinAcc<F>& a) {
+  uint32_t k32[F::L], k64[F::L];
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    k32[l] = 2u * F::P16[l];
+    k64[l] = 4u * F::P16[l];
+  }
+  F29<F> r = f29_sub<F>(lin_carry<F>(a.pos), lin_carry<F>(a.neg), k32);
+  r = f29_csub<F>(r, k64);
+  r = f29_csub<F>(r, k32);
+  r = f29_csub<F>(r, F::P16);
+  r = f29_csub<F>(r, F::P8);
+  r = f29_csub<F>(r, F::P4);
+  return f29_csub<F>(r, F::P2);
+}
+
 // Karatsuba parts of an Fp2 product x y: 0 = xa ya, 1 = xb yb,
 // 2 = (xa + xb)(ya + yb); the product is (p0 - p1, p2 - p0 - p1) and xi
 // times it (2 p0 - p2, p2 - 2 p1)
@@ -964,6 +1058,336 @@ KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
   if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C>(f, f);
 }
 
+// The same line table for a variable Q with the G2 chain spread over a wave
+// (k_vlines runs it on one lane: ~25 dependent Fp2 operations per step).
+// Each step is a few rounds of independent Fp2 products, one Karatsuba part
+// per lane, folded lazily (LinAcc):
+//   doubling (dbl-2009-l + tangent):  [X^2, Y^2, Z^2, YZ] -> [2YZ ZZ, E ZZ, E X, B^2,
+//                                     (X+B)^2, E^2] -> [E (D - X3)]
+//   addition (madd-2007-bl + chord): [Z^2] -> [qx Z1Z1, Z Z1Z1] -> [qy ZZZ, H^2, Z H]
+//                                     -> [H I, X I, r^2, r qx, qy Z3] -> [Y J, r (V - X3)]
+// Any Jacobian representative gives the lines up to Fp2 factors, which the
+// final exponentiation removes.  T = O or H = 0 (impossible for Q of order
+// r) sets redo[q]; k_vlines_redo then recomputes that table on one lane.
+template <class C>
+struct VLine {
+  static constexpr int L = C::Fp29::L, E2 = 2 * L;
+  // Fp2 slots
+  enum { X, Y, Z, QX, QY, Q1X, Q1Y, Q2X, Q2Y, A, B, ZZ, YZ, D, CC, Z1Z1, U2, ZZZ, H, R, Z3, I, J, V, NS };
+  static constexpr int PROD = NS * E2;  // 18 parts of L words
+  static constexpr int FLAG = PROD + 18 * L;
+  static constexpr int WORDS = FLAG + 4;
+};
+
+template <class C>
+KZGX_DEV uint32_t* vl_slot(int k) {
+  return vw_smem + k * VLine<C>::E2;
+}
+// lanes < 3 n: part (lane % 3) of product lane / 3, operands from `ops`
+template <class C, class Ops>
+KZGX_DEV void vl_parts(int n, Ops ops) {
+  const int lane = threadIdx.x;
+  if (lane < 3 * n) {
+    Fp2<C> x, y;
+    ops(lane / 3, x, y);
+    vw_st<C>(vw_smem + VLine<C>::PROD + lane * VLine<C>::L, vw_part<C>(x, y, lane % 3));
+  }
+  __syncthreads();
+}
+template <class C>
+KZGX_DEV const uint32_t* vl_prod(int k) {
+  return vw_smem + VLine<C>::PROD + 3 * k * VLine<C>::L;
+}
+template <class C>
+KZGX_DEV const uint32_t* vl_comp(int slot, int im) {
+  return vw_smem + slot * VLine<C>::E2 + im * VLine<C>::L;
+}
+
+template <class C>
+KZGX_DEV void vl_dbl_wave(uint32_t* out) {
+  using F = typename C::Fp29;
+  using S = VLine<C>;
+  constexpr int L = S::L, E2 = S::E2;
+  const int lane = threadIdx.x;
+  // round 1: A = X^2, B = Y^2, ZZ = Z^2, YZ = Y Z
+  vl_parts<C>(4, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const int a = k == 0 ? S::X : k == 1 ? S::Y : k == 2 ? S::Z : S::Y;
+    const int b = k == 3 ? S::Z : a;
+    x = vw_ld2<C>(vl_slot<C>(a));
+    y = vw_ld2<C>(vl_slot<C>(b));
+  });
+  if (lane < 8) {
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(k), im, false, 1);
+    const int dst = k == 0 ? S::A : k == 1 ? S::B : k == 2 ? S::ZZ : S::YZ;
+    vw_st<C>(vl_slot<C>(dst) + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  // round 2: 2YZ ZZ, E ZZ, E X, B^2, (X + B)^2, E^2 with E = 3A
+  vl_parts<C>(6, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+    const Fp2<C> E = f2_add<C>(f2_dbl<C>(a), a);
+    if (k == 0) {
+      x = f2_dbl<C>(vw_ld2<C>(vl_slot<C>(S::YZ)));
+      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+    } else if (k == 1) {
+      x = E;
+      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+    } else if (k == 2) {
+      x = E;
+      y = vw_ld2<C>(vl_slot<C>(S::X));
+    } else if (k == 3) {
+      x = y = vw_ld2<C>(vl_slot<C>(S::B));
+    } else if (k == 4) {
+      x = y = f2_add<C>(vw_ld2<C>(vl_slot<C>(S::X)), vw_ld2<C>(vl_slot<C>(S::B)));
+    } else {
+      x = y = E;
+    }
+  });
+  // w0c = P0, w1c = -P1, w3c = P2 - 2B, C = P3, D = 2 P4 - 2A - 2 P3,
+  // X3 = P5 - 2D = P5 - 4 P4 + 4A + 4 P3, Z3 = 2 YZ
+  if (lane < 14) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    switch (w) {
+      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -1); break;
+      case 2:
+        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
+        lin_add<F>(acc, vl_comp<C>(S::B, im), -2);
+        break;
+      case 3: lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1); break;
+      case 4:
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, 2);
+        lin_add<F>(acc, vl_comp<C>(S::A, im), -2);
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, -2);
+        break;
+      case 5:
+        lin_add_f2<F>(acc, vl_prod<C>(5), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -4);
+        lin_add<F>(acc, vl_comp<C>(S::A, im), 4);
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 4);
+        break;
+      default: lin_add<F>(acc, vl_comp<C>(S::YZ, im), 2); break;
+    }
+    const F29<F> v = lin_fin_wide<F>(acc);
+    if (w < 3) {
+      vw_st<C>(out + w * E2 + im * L, v);
+    } else {
+      const int dst = w == 3 ? S::CC : w == 4 ? S::D : w == 5 ? S::X : S::Z;
+      vw_st<C>(vl_slot<C>(dst) + im * L, v);
+    }
+  }
+  __syncthreads();
+  // round 3: Y3 = E (D - X3) - 8 C
+  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+    x = f2_add<C>(f2_dbl<C>(a), a);
+    y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::D)), vw_ld2<C>(vl_slot<C>(S::X)));
+  });
+  if (lane < 2) {
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(0), lane, false, 1);
+    lin_add<F>(acc, vl_comp<C>(S::CC, lane), -8);
+    vw_st<C>(vl_slot<C>(S::Y) + lane * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::Z)))) vw_smem[S::FLAG] = 1u;  // T = O
+  __syncthreads();
+}
+
+// T += q (q = slots qx, qy) and the chord line into out
+template <class C>
+KZGX_DEV void vl_add_wave(int qx, int qy, uint32_t* out) {
+  using F = typename C::Fp29;
+  using S = VLine<C>;
+  constexpr int L = S::L, E2 = S::E2;
+  const int lane = threadIdx.x;
+  auto fin1 = [&](int k, int dst, int d) {  // lanes 2k, 2k+1: slot dst = d * product k
+    if ((lane >> 1) == k) {
+      LinAcc<F> acc;
+      lin_init<F>(acc);
+      lin_add_f2<F>(acc, vl_prod<C>(k), lane & 1, false, d);
+      vw_st<C>(vl_slot<C>(dst) + (lane & 1) * L, lin_fin<F>(acc));
+    }
+  };
+  // Z1Z1 = Z^2
+  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) { x = y = vw_ld2<C>(vl_slot<C>(S::Z)); });
+  fin1(0, S::Z1Z1, 1);
+  __syncthreads();
+  // U2 = qx Z1Z1, ZZZ = Z Z1Z1
+  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qx : S::Z));
+    y = vw_ld2<C>(vl_slot<C>(S::Z1Z1));
+  });
+  fin1(0, S::U2, 1);
+  fin1(1, S::ZZZ, 1);
+  __syncthreads();
+  if (lane < 2) {  // H = U2 - X
+    const int im = lane;
+    vw_st<C>(vl_slot<C>(S::H) + im * L, fp_sub<F>(vw_ld<C>(vl_comp<C>(S::U2, im)), vw_ld<C>(vl_comp<C>(S::X, im))));
+  }
+  __syncthreads();
+  // S2 = qy ZZZ, HH = H^2, ZH = Z H
+  vl_parts<C>(3, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qy : k == 1 ? S::H : S::Z));
+    y = vw_ld2<C>(vl_slot<C>(k == 0 ? S::ZZZ : S::H));
+  });
+  // r = 2 (S2 - Y), I = 4 HH, Z3 = 2 ZH
+  if (lane < 6) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(w), im, false, w == 1 ? 4 : 2);
+    if (w == 0) lin_add<F>(acc, vl_comp<C>(S::Y, im), -2);
+    vw_st<C>(vl_slot<C>(w == 0 ? S::R : w == 1 ? S::I : S::Z3) + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::H)))) vw_smem[S::FLAG] = 1u;  // T = +-q
+  // J = H I, V = X I, r^2, r qx, qy Z3
+  vl_parts<C>(5, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const int a = k == 0 ? S::H : k == 1 ? S::X : k == 4 ? qy : S::R;
+    const int b = k <= 1 ? S::I : k == 2 ? S::R : k == 3 ? qx : S::Z3;
+    x = vw_ld2<C>(vl_slot<C>(a));
+    y = vw_ld2<C>(vl_slot<C>(b));
+  });
+  // J, V; X3 = r^2 - J - 2V; line: w0c = Z3, w1c = -r, w3c = r qx - qy Z3
+  if (lane < 12) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    switch (w) {
+      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, 1); break;
+      case 2:
+        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(0), im, false, -1);
+        lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+        break;
+      case 3: lin_add<F>(acc, vl_comp<C>(S::Z3, im), 1); break;
+      case 4: lin_add<F>(acc, vl_comp<C>(S::R, im), -1); break;
+      default:
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -1);
+        break;
+    }
+    const F29<F> v = lin_fin<F>(acc);
+    if (w < 3)
+      vw_st<C>(vl_slot<C>(w == 0 ? S::J : w == 1 ? S::V : S::D) + im * L, v);  // D holds X3 for now
+    else
+      vw_st<C>(out + (w - 3) * E2 + im * L, v);
+  }
+  __syncthreads();
+  // Y3 = r (V - X3) - 2 Y J
+  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    if (k == 0) {
+      x = vw_ld2<C>(vl_slot<C>(S::R));
+      y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::V)), vw_ld2<C>(vl_slot<C>(S::D)));
+    } else {
+      x = vw_ld2<C>(vl_slot<C>(S::Y));
+      y = vw_ld2<C>(vl_slot<C>(S::J));
+    }
+  });
+  if (lane < 6) {  // new T: X = X3, Y = Y3, Z = Z3
+    const int w = lane >> 1, im = lane & 1;
+    F29<F> v;
+    if (w == 0) {
+      v = vw_ld<C>(vl_comp<C>(S::D, im));
+    } else if (w == 1) {
+      LinAcc<F> acc;
+      lin_init<F>(acc);
+      lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1);
+      lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+      v = lin_fin<F>(acc);
+    } else {
+      v = vw_ld<C>(vl_comp<C>(S::Z3, im));
+    }
+    vw_st<C>(vl_slot<C>(w) + im * L, v);  // slots X, Y, Z are 0, 1, 2
+  }
+  __syncthreads();
+}
+
+// block q: the line table of Q_q (canonical) into lines + q NL LW
+template <class C>
+__global__ __launch_bounds__(64) void k_vlines_wave(const uint32_t* __restrict__ g2, uint32_t* __restrict__ lines,
+                                                    uint32_t* __restrict__ qfin, uint32_t* __restrict__ redo) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  using S = VLine<C>;
+  const int q = blockIdx.x;
+  uint32_t* out = lines + (size_t)q * V::NL * V::LW;
+  if (threadIdx.x == 0) {
+    G2A<C> Q;
+    const bool fin = g2_from_canon<C>(g2 + q * 4 * C::Fp::N, Q);
+    qfin[q] = fin ? 1u : 0u;
+    redo[q] = 0u;
+    vw_smem[S::FLAG] = fin ? 0u : 2u;
+    vw_st2<C>(vl_slot<C>(S::X), Q.x);
+    vw_st2<C>(vl_slot<C>(S::Y), Q.y);
+    vw_st2<C>(vl_slot<C>(S::Z), f2_one<C>());
+    vw_st2<C>(vl_slot<C>(S::QX), Q.x);
+    vw_st2<C>(vl_slot<C>(S::QY), Q.y);
+    if (P::D_TWIST) {
+      const G2A<C> q1 = twist_frob<C>(Q);
+      G2A<C> q2 = twist_frob<C>(q1);
+      q2.y = f2_neg<C>(q2.y);
+      vw_st2<C>(vl_slot<C>(S::Q1X), q1.x);
+      vw_st2<C>(vl_slot<C>(S::Q1Y), q1.y);
+      vw_st2<C>(vl_slot<C>(S::Q2X), q2.x);
+      vw_st2<C>(vl_slot<C>(S::Q2Y), q2.y);
+    }
+  }
+  __syncthreads();
+  if (vw_smem[S::FLAG] == 2u) return;  // Q = O: no table (uniform)
+  int s = 0;
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    vl_dbl_wave<C>(out + (s++) * V::LW);
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) vl_add_wave<C>(S::QX, S::QY, out + (s++) * V::LW);
+  }
+  if (P::LOOP_NEG && threadIdx.x < 2) {
+    using F = typename C::Fp29;
+    uint32_t* y = vl_slot<C>(S::Y) + threadIdx.x * S::L;
+    vw_st<C>(y, fp_neg<F>(vw_ld<C>(y)));
+  }
+  __syncthreads();
+  if (P::D_TWIST) {
+    vl_add_wave<C>(S::Q1X, S::Q1Y, out + (s++) * V::LW);
+    vl_add_wave<C>(S::Q2X, S::Q2Y, out + (s++) * V::LW);
+  }
+  if (threadIdx.x == 0 && vw_smem[S::FLAG]) redo[q] = 1u;
+}
+
+// single-lane recompute of the tables flagged by k_vlines_wave
+template <class C>
+__global__ __launch_bounds__(64) void k_vlines_redo(const uint32_t* __restrict__ g2, uint32_t* __restrict__ lines,
+                                                    const uint32_t* __restrict__ redo) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  const int q = threadIdx.x;
+  if (q >= 2 || !redo[q]) return;
+  G2A<C> Q;
+  (void)g2_from_canon<C>(g2 + q * 4 * C::Fp::N, Q);
+  uint32_t* out = lines + (size_t)q * V::NL * V::LW;
+  int s = 0;
+  G2J<C> T = g2_from_affine<C>(Q);
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    vl_dbl<C>(T, out + (s++) * V::LW);
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) vl_add<C>(T, Q, out + (s++) * V::LW);
+  }
+  if (P::LOOP_NEG) T.Y = f2_neg<C>(T.Y);
+  if (P::D_TWIST) {
+    const G2A<C> q1 = twist_frob<C>(Q);
+    G2A<C> q2 = twist_frob<C>(q1);
+    q2.y = f2_neg<C>(q2.y);
+    vl_add<C>(T, q1, out + (s++) * V::LW);
+    vl_add<C>(T, q2, out + (s++) * V::LW);
+  }
+}
+
 // the product of the two pairings (P_q, Q_q), q = 0, 1, from the line tables
 // of Q_0, Q_1 (k_vlines) and the per-pairing scale factors and use flags the
 // caller left in LDS (scale: [q][yP, xP, 1] up to an Fp factor; flag[q]);
@@ -1142,6 +1566,46 @@ int gen_srs_g2_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, u
 }
 
 template <class C>
+static int msm_g2_windowed(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, const uint32_t* d_tab,
+                           size_t n, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  const size_t m = n * G2_TAB_W;
+  const size_t tb = (m + m / 8 + 64) * sizeof(G2J<C>);
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_g2_ws, tb, &ctx->g2_ws_b));
+  G2J<C>* a = (G2J<C>*)ctx->d_g2_ws;
+  G2J<C>* b = a + m;
+  {
+    ProfScope p(ctx, st, "g2_terms");
+    hipLaunchKernelGGL(k_g2_terms_w<C>, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, st, d_scalars, d_srs2,
+                       (const G2A<C>*)d_tab, (uint32_t)n, a);
+  }
+  size_t cnt = m;
+  while (cnt > 64) {
+    const size_t nxt = (cnt + 7) / 8;
+    hipLaunchKernelGGL(k_g2_fold8<C>, dim3((unsigned)((nxt + 63) / 64)), dim3(64), 0, st, a, (uint32_t)cnt, b);
+    std::swap(a, b);
+    cnt = nxt;
+  }
+  hipLaunchKernelGGL(k_g2_sum_tree<C>, dim3(1), dim3(64), 0, st, a, (uint32_t)cnt, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+size_t g2_table_bytes(int curve, size_t n) {
+  return n * G2_TAB_W * (curve == KZGX_CURVE_BN254 ? sizeof(G2A<BN254G1>) : sizeof(G2A<BLS12381G1>));
+}
+
+int g2_table_build(Ctx* ctx, const uint32_t* d_srs2, size_t n, uint32_t* d_tab, hipStream_t st) {
+  dim3 blk(64), grd((unsigned)((n + 63) / 64));
+  ProfScope p(ctx, st, "g2_table");
+  if (ctx->curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g2_tab<BN254G1>, grd, blk, 0, st, d_srs2, (uint32_t)n, (G2A<BN254G1>*)d_tab);
+  else
+    hipLaunchKernelGGL(k_g2_tab<BLS12381G1>, grd, blk, 0, st, d_srs2, (uint32_t)n, (G2A<BLS12381G1>*)d_tab);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+template <class C>
 static int msm_g2_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
                        uint32_t* d_out_inf, hipStream_t st) {
   const size_t tb = (n + 64) * sizeof(G2J<C>);
@@ -1159,7 +1623,7 @@ static int msm_g2_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_sr
 }
 
 int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
-           uint32_t* d_out_inf, hipStream_t st) {
+           uint32_t* d_out_inf, hipStream_t st, const uint32_t* d_tab) {
   if (n == 0) {  // ECP2_inf (trusted_setup.cpp:177-181)
     const size_t pb = 4 * (size_t)ctx->base_words() * 4;
     KZGX_TRY_HIP(hipMemsetAsync(d_out, 0, pb, st));
@@ -1168,6 +1632,10 @@ int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n
     KZGX_TRY_HIP(hipStreamSynchronize(st));
     return KZGX_OK;
   }
+  if (d_tab)
+    return ctx->curve == KZGX_CURVE_BN254
+               ? msm_g2_windowed<BN254G1>(ctx, d_scalars, d_srs2, d_tab, n, d_out, d_out_inf, st)
+               : msm_g2_windowed<BLS12381G1>(ctx, d_scalars, d_srs2, d_tab, n, d_out, d_out_inf, st);
   return ctx->curve == KZGX_CURVE_BN254 ? msm_g2_impl<BN254G1>(ctx, d_scalars, d_srs2, n, d_out, d_out_inf, st)
                                         : msm_g2_impl<BLS12381G1>(ctx, d_scalars, d_srs2, n, d_out, d_out_inf, st);
 }
@@ -1257,7 +1725,8 @@ template <class C>
 static int pair2_wave_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
                            uint32_t* d_lines, uint32_t* d_ok, hipStream_t st) {
   uint32_t* qfin = d_lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
-  hipLaunchKernelGGL(k_vlines<C>, dim3(1), dim3(64), 0, st, d_q, d_lines, qfin);
+  hipLaunchKernelGGL(k_vlines_wave<C>, dim3(2), dim3(64), VLine<C>::WORDS * 4, st, d_q, d_lines, qfin, qfin + 2);
+  hipLaunchKernelGGL(k_vlines_redo<C>, dim3(1), dim3(64), 0, st, d_q, d_lines, qfin + 2);
   hipLaunchKernelGGL(k_pair2_wave<C>, dim3(1), dim3(64), VWave<C>::WORDS * 4, st, d_p, d_p_inf, d_q_inf, d_lines,
                      qfin, d_ok);
   KZGX_TRY_HIP(hipGetLastError());
