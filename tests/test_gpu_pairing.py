@@ -127,6 +127,25 @@ def test_msm_g2_matches_naive(name, C, ctxs):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
+def test_msm_g2_windowed_edges(name, C, ctxs):
+    """the windowed G2 table path: tau = 0 leaves G2[i >= 1] at infinity; scalars with
+    all-zero 16-bit windows, a single set bit per window and r - 1"""
+    ctx = ctxs(name)
+    n = 6
+    ctx.gen_srs_g2(0, n)
+    srs2 = PR.gen_srs_g2(C, 0, n)
+    sc = [C.r - 1, 7, 0, 1 << 200, 3, 5]
+    out, inf = ctx.msm_g2(scalars(sc))
+    assert g2_from_row(C, out, inf) == PR.polyeval_g2(C, srs2, sc)
+    tau = K.default_tau(C)
+    ctx.gen_srs_g2(tau, n)
+    srs2 = PR.gen_srs_g2(C, tau, n)
+    sc = [sum(1 << (16 * w + (w % 16)) for w in range(15)), (1 << 16) - 1, 1 << 240, 0, C.r - 2, 65536]
+    out, inf = ctx.msm_g2(scalars(sc))
+    assert g2_from_row(C, out, inf) == PR.polyeval_g2(C, srs2, sc)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
 def test_pairing_matches_oracle(name, C, ctxs):
     ctx = ctxs(name)
     G1, G2 = (C.gx, C.gy), PR.g2_generator(C)
