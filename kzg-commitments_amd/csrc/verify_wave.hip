@@ -1,0 +1,1157 @@
+// Wave-per-opening verify on gfx950: the two-pairing product check of
+// verify_proof (reference src/trusted_setup.cpp:230-254) with every Fp12
+// product spread over a 64-lane wave, the G2 line tables it consumes, and
+// the wave-parallel G2 chain for a variable second argument.  Split from
+// pairing.hip to keep each translation unit's compile time bounded.
+#include <hip/hip_runtime.h>
+
+#include "pairing_common.hpp"
+
+namespace kzgx {
+
+// ---- wave-parallel single verify (latency path) ----------------------------------
+// One 64-lane wave per opening instead of one lane: the same product of two
+// Miller loops and one final exponentiation as k_verify_single, with every
+// Fp12 product spread over the wave.  Fp12 is kept in the w basis
+// (a = sum_k a_k w^k, a_k in Fp2, w^6 = xi; tower c_h.c_j is w^(2j+h)) in
+// LDS: a dense product is 36 Fp2 products, one per lane, then 12 lanes fold
+// the columns; a line product is 18 Fp2 products and 3-term folds.
+// Both G2 arguments are fixed by the setup (G2[0], G2[1] = [tau]G2), so
+// their line coefficients are precomputed once (k_vlines) and only scaled
+// by the G1 argument's coordinates per opening; the G1 argument -D is used
+// in XYZZ form (the line is multiplied by the Fp factor ZZ ZZZ, which the
+// final exponentiation removes).  [y]G comes from a table of
+// d 2^(8w) G (k_vtab: 32 windows x 255 digits) summed by a 5-level tree;
+// [z]pi is double-and-add over z's bit length (z is a point index in the
+// reference's use, trusted_setup.cpp:230-254).
+#ifdef KZGX_VW_TIMING
+#define VW_STAMP(i) \
+  if (threadIdx.x == 0) vw_ts[i] = wall_clock64()
+__device__ uint64_t vw_ts[16];
+#else
+#define VW_STAMP(i)
+#endif
+
+template <class C>
+struct VWave {
+  using P = typename PairOf<C>::T;
+  static constexpr int L = C::Fp29::L;
+  static constexpr int E2 = 2 * L;    // words per Fp2
+  static constexpr int E12 = 12 * L;  // words per Fp12 (6 Fp2)
+  static constexpr int LW = 3 * E2;   // words per line (w0, w1, w3 coefficients)
+  static constexpr int adds_below_top() {
+    int n = 0;
+    for (int i = 0; i < P::LOOP_BITS - 1; i++) n += (int)((P::LOOP[i >> 6] >> (i & 63)) & 1ull);
+    return n;
+  }
+  static constexpr int NL = (P::LOOP_BITS - 1) + adds_below_top() + (P::D_TWIST ? 2 : 0);
+  static constexpr int TAB = 32 * 255;  // [y]G table entries
+  static constexpr int AW = affine_words<C>();
+  // positions of the w0, w1, w3 coefficients in the w basis
+  static constexpr int POS0 = P::D_TWIST ? 0 : 3, POS1 = P::D_TWIST ? 1 : 2, POS3 = P::D_TWIST ? 3 : 0;
+  static constexpr int NSLOT = 9;
+  // LDS carve (words)
+  static constexpr int O_LINES = 0;                        // [2][NL][LW] scaled lines
+  static constexpr int O_SLOT = O_LINES + 2 * NL * LW;     // [NSLOT][E12]
+  static constexpr int O_PROD = O_SLOT + NSLOT * E12;      // [36][E2] products; G1 phase: [32][4L] XYZZ tree
+  static constexpr int PROD_W = (36 * E2 > 32 * 4 * L) ? 36 * E2 : 32 * 4 * L;
+  static constexpr int O_SCALE = O_PROD + PROD_W;          // [2][3][L] scale factors
+  static constexpr int O_FLAG = O_SCALE + 6 * L;           // [16]
+  static constexpr int WORDS = O_FLAG + 16;
+};
+
+// the wave kernel's LDS (dynamic; V::WORDS words), addressed by word offset
+// so that the non-inlined helpers still issue LDS (ds_*) instructions
+extern __shared__ __attribute__((aligned(16))) uint32_t vw_smem[];
+
+template <class C>
+KZGX_DEV F29<typename C::Fp29> vw_ld(const uint32_t* p) {
+  F29<typename C::Fp29> r;
+#pragma unroll
+  for (int i = 0; i < C::Fp29::L; i++) r.v[i] = p[i];
+  return r;
+}
+template <class C>
+KZGX_DEV void vw_st(uint32_t* p, const F29<typename C::Fp29>& a) {
+#pragma unroll
+  for (int i = 0; i < C::Fp29::L; i++) p[i] = a.v[i];
+}
+template <class C>
+KZGX_DEV Fp2<C> vw_ld2(const uint32_t* p) {
+  return Fp2<C>{vw_ld<C>(p), vw_ld<C>(p + C::Fp29::L)};
+}
+template <class C>
+KZGX_DEV void vw_st2(uint32_t* p, const Fp2<C>& a) {
+  vw_st<C>(p, a.a);
+  vw_st<C>(p + C::Fp29::L, a.b);
+}
+
+// line coefficients of the Miller loop for a fixed Q, in consumption order:
+// (w0c, w1c, w3c) with the line at P = w0c yP, w1c xP, w3c (line_dbl /
+// line_add with the P factors left out)
+template <class C>
+KZGX_DEV void vl_dbl(G2J<C>& T, uint32_t* out) {
+  constexpr int E2 = VWave<C>::E2;
+  const Fp2<C> A = f2_sqr<C>(T.X);
+  const Fp2<C> B = f2_sqr<C>(T.Y);
+  const Fp2<C> E = f2_add<C>(f2_dbl<C>(A), A);
+  const Fp2<C> ZZ = f2_sqr<C>(T.Z);
+  const Fp2<C> Z3 = f2_dbl<C>(f2_mul<C>(T.Y, T.Z));
+  vw_st2<C>(out, f2_mul<C>(Z3, ZZ));
+  vw_st2<C>(out + E2, f2_neg<C>(f2_mul<C>(E, ZZ)));
+  vw_st2<C>(out + 2 * E2, f2_sub<C>(f2_mul<C>(E, T.X), f2_dbl<C>(B)));
+  T = g2_dbl<C>(T);
+}
+template <class C>
+KZGX_DEV void vl_add(G2J<C>& T, const G2A<C>& q, uint32_t* out) {
+  constexpr int E2 = VWave<C>::E2;
+  const Fp2<C> Z1Z1 = f2_sqr<C>(T.Z);
+  const Fp2<C> U2 = f2_mul<C>(q.x, Z1Z1);
+  const Fp2<C> S2 = f2_mul<C>(q.y, f2_mul<C>(T.Z, Z1Z1));
+  const Fp2<C> H = f2_sub<C>(U2, T.X);
+  const Fp2<C> rr = f2_dbl<C>(f2_sub<C>(S2, T.Y));
+  const Fp2<C> Z3 = f2_dbl<C>(f2_mul<C>(T.Z, H));
+  vw_st2<C>(out, Z3);
+  vw_st2<C>(out + E2, f2_neg<C>(rr));
+  vw_st2<C>(out + 2 * E2, f2_sub<C>(f2_mul<C>(rr, q.x), f2_mul<C>(q.y, Z3)));
+  T = g2_add_mixed<C>(T, q);
+}
+
+// lanes 0, 1: the line tables of Q0 = G2[0] and Q1 = G2[1]; qfin[q] = finite
+template <class C>
+__global__ __launch_bounds__(64) void k_vlines(const uint32_t* __restrict__ g2_01, uint32_t* __restrict__ lines,
+                                               uint32_t* __restrict__ qfin) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  const int q = threadIdx.x;
+  if (q >= 2) return;
+  G2A<C> Q;
+  const bool fin = g2_from_canon<C>(g2_01 + q * 4 * C::Fp::N, Q);
+  qfin[q] = fin ? 1u : 0u;
+  if (!fin) return;
+  uint32_t* out = lines + (size_t)q * V::NL * V::LW;
+  int s = 0;
+  G2J<C> T = g2_from_affine<C>(Q);
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    vl_dbl<C>(T, out + (s++) * V::LW);
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) vl_add<C>(T, Q, out + (s++) * V::LW);
+  }
+  if (P::LOOP_NEG) T.Y = f2_neg<C>(T.Y);
+  if (P::D_TWIST) {
+    const G2A<C> q1 = twist_frob<C>(Q);
+    G2A<C> q2 = twist_frob<C>(q1);
+    q2.y = f2_neg<C>(q2.y);
+    vl_add<C>(T, q1, out + (s++) * V::LW);
+    vl_add<C>(T, q2, out + (s++) * V::LW);
+  }
+}
+
+// entry (w, d - 1) = d 2^(8 w) G for d in 1..255 (affine Montgomery)
+template <class C>
+__global__ __launch_bounds__(64) void k_vtab(const uint32_t* __restrict__ g1_0, uint32_t* __restrict__ tab) {
+  using V = VWave<C>;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)V::TAB) return;
+  const uint32_t w = t / 255, d = t % 255 + 1;
+  Affine<C> g;
+  (void)affine_from_canonical<C>(g1_0, g);
+  uint32_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  e[w >> 2] = d << (8 * (w & 3));
+  Affine<C> a;
+  if (!xyzz_to_affine<C>(g1_mul_words<C>(g, e), a)) a.x = a.y = f29_zero<typename C::Fp29>();
+  affine_store<C>(tab + (size_t)t * V::AW, a);
+}
+
+// Lazy signed combination sum_j c_j p_j of values < 2m with normalized
+// limbs and small integer c_j: the positive and negative parts accumulate
+// limb-wise in 64 bits (one v_mad_u64_u32 per limb and sign), then one
+// carry pass each, one subtraction and a csub chain.  This replaces a
+// carried, reduced add per term (the bulk of a round's instructions).
+// Bounds: sum of positive c_j <= 16 and of negative |c_j| <= 16 -> the
+// difference + 32m lies in [0, 64m), reduced to < 2m.
+template <class F>
+struct LinAcc {
+  uint64_t pos[F::L], neg[F::L];
+};
+template <class F>
+KZGX_DEV void lin_init(LinAcc<F>& a) {
+#pragma unroll
+  for (int l = 0; l < F::L; l++) a.pos[l] = a.neg[l] = 0;
+}
+template <class F>
+KZGX_DEV void lin_add(LinAcc<F>& a, const uint32_t* p, int c) {
+  const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    const uint32_t x = p[l];
+    a.pos[l] += (uint64_t)x * cp;
+    a.neg[l] += (uint64_t)x * cn;
+  }
+}
+template <class F>
+KZGX_DEV void lin_add(LinAcc<F>& a, const F29<F>& p, int c) {
+  lin_add<F>(a, p.v, c);
+}
+template <class F>
+KZGX_DEV F29<F> lin_carry(const uint64_t (&v)[F::L]) {
+  F29<F> r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    const uint64_t t = v[l] + c;
+    r.v[l] = l + 1 < F::L ? ((uint32_t)t & M29) : (uint32_t)t;
+    c = t >> 29;
+  }
+  return r;
+}
+template <class F>
+KZGX_DEV F29<F> lin_fin(const LinAcc<F>& a) {
+  uint32_t k32[F::L];
+#pragma unroll
+  for (int l = 0; l < F::L; l++) k32[l] = 2u * F::P16[l];  // 32m, limbs < 2^30
+  F29<F> r = f29_sub<F>(lin_carry<F>(a.pos), lin_carry<F>(a.neg), k32);
+  r = f29_csub<F>(r, k32);
+  r = f29_csub<F>(r, F::P16);
+  r = f29_csub<F>(r, F::P8);
+  r = f29_csub<F>(r, F::P4);
+  return f29_csub<F>(r, F::P2);
+}
+
+// ---- Fp12 (w basis) in LDS, wave-cooperative; every op ends with a barrier
+// dst = a b (dst may alias a or b)
+template <class C>
+KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o) {
+  uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
+  const uint32_t *a = vw_smem + a_o, *b = vw_smem + b_o;
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  const int lane = threadIdx.x;
+  if (lane < 36) {
+    const int i = lane / 6, j = lane % 6;
+    vw_st2<C>(prod + lane * E2, f2_mul<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(b + j * E2)));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij,  xi (t0 + t1 i) = (t0 - t1) + (t0 + t1) i
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    for (int i = 0; i < 6; i++) {
+      const int j = k - i;
+      if (j >= 0) lin_add<F>(acc, prod + (i * 6 + j) * E2 + im * L, 1);
+      const int j2 = k + 6 - i;
+      if (j2 < 6) {
+        const uint32_t* p = prod + (i * 6 + j2) * E2;
+        lin_add<F>(acc, p, 1);
+        lin_add<F>(acc, p + L, im ? 1 : -1);
+      }
+    }
+    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+}
+
+// as lin_fin for positive parts up to 32 units (value < 64m + 32m)
+template <class F>
+KZGX_DEV F29<F> lin_fin_wide(const LinAcc<F>& a) {
+  uint32_t k32[F::L], k64[F::L];
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    k32[l] = 2u * F::P16[l];
+    k64[l] = 4u * F::P16[l];
+  }
+  F29<F> r = f29_sub<F>(lin_carry<F>(a.pos), lin_carry<F>(a.neg), k32);
+  r = f29_csub<F>(r, k64);
+  r = f29_csub<F>(r, k32);
+  r = f29_csub<F>(r, F::P16);
+  r = f29_csub<F>(r, F::P8);
+  r = f29_csub<F>(r, F::P4);
+  return f29_csub<F>(r, F::P2);
+}
+
+// Karatsuba parts of an Fp2 product x y: 0 = xa ya, 1 = xb yb,
+// 2 = (xa + xb)(ya + yb); the product is (p0 - p1, p2 - p0 - p1) and xi
+// times it (2 p0 - p2, p2 - 2 p1)
+template <class C>
+KZGX_DEV F29<typename C::Fp29> vw_part(const Fp2<C>& X, const Fp2<C>& Y, int part) {
+  using F = typename C::Fp29;
+  F29<F> o0 = X.a, o1 = Y.a;
+  if (part == 1) {
+    o0 = X.b;
+    o1 = Y.b;
+  } else if (part == 2) {
+    o0 = f29_add<F>(X.a, X.b);  // < 4m: the product stays < 16 m^2
+    o1 = f29_add<F>(Y.a, Y.b);
+  }
+  return f29_mul<F>(o0, o1);
+}
+// add d (x product) or d (xi x product) of parts q[0..2], component im
+template <class F>
+KZGX_DEV void lin_add_f2(LinAcc<F>& acc, const uint32_t* q, int im, bool xi, int d) {
+  constexpr int L = F::L;
+  // coefficients of (p0, p1, p2): re (1, -1, 0), im (-1, -1, 1); xi: re (2, 0, -1), im (0, -2, 1)
+  const int c0 = xi ? (im ? 0 : 2) : (im ? -1 : 1);
+  const int c1 = xi ? (im ? -2 : 0) : -1;
+  const int c2 = xi ? (im ? 1 : -1) : (im ? 1 : 0);
+  lin_add<F>(acc, q, d * c0);
+  lin_add<F>(acc, q + L, d * c1);
+  lin_add<F>(acc, q + 2 * L, d * c2);
+}
+
+// f = f l for a scaled line l = (l0, l1, l3) at positions (POS0, POS1, POS3):
+// 18 Fp2 products f_i l_t as 54 Fp (Karatsuba) parts, one per lane, then
+// lane (k, im) < 12 folds the three products landing on w^k (xi for the
+// wrapped ones) lazily
+template <class C>
+KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int E2 = V::E2, L = V::L;
+  uint32_t *f = vw_smem + f_o, *prod = vw_smem + prod_o;
+  const uint32_t* line = vw_smem + line_o;
+  const int lane = threadIdx.x;
+  if (lane < 54) {
+    const int i = lane / 9, t = (lane / 3) % 3;
+    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(f + i * E2), vw_ld2<C>(line + t * E2), lane % 3));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      const int pos = t == 0 ? V::POS0 : t == 1 ? V::POS1 : V::POS3;
+      int i = k - pos;
+      const bool wrap = i < 0;
+      if (wrap) i += 6;
+      lin_add_f2<F>(acc, prod + (i * 9 + t * 3) * L, im, wrap, 1);
+    }
+    vw_st<C>(f + k * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+}
+
+// dst = a^2 for any a: the 21 products a_i a_j (i <= j) as 63 Fp
+// (Karatsuba) parts, one per lane; lane (k, im) < 12 folds the pairs with
+// i + j = k and, times xi, i + j = k + 6 (cross terms doubled)
+template <class C>
+KZGX_DEV int vw_pair_index(int i, int j) {
+  return i * 6 - (i * (i - 1)) / 2 + (j - i);
+}
+template <class C>
+KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
+  const uint32_t* a = vw_smem + a_o;
+  const int lane = threadIdx.x;
+  if (lane < 63) {
+    int idx = lane / 3, i = 0;
+    while (idx >= 6 - i) {
+      idx -= 6 - i;
+      i++;
+    }
+    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(a + (i + idx) * E2), lane % 3));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    for (int w = 0; w < 2; w++) {
+      const int sum = k + 6 * w;
+      for (int i = 0; i < 6; i++) {
+        const int j = sum - i;
+        if (j < i || j > 5) continue;
+        lin_add_f2<F>(acc, prod + 3 * vw_pair_index<C>(i, j) * L, im, w == 1, i != j ? 2 : 1);
+      }
+    }
+    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+}
+
+// Granger-Scott squaring of a cyclotomic element (f12_cyclo_sqr) with one Fp
+// product per lane.  In the w basis the three Fp4 squarings pair (a_j, a_{j+3}),
+// j = 0, 1, 2: fp4_sqr(x, y) needs t = x y and u = (x + y)(x + xi y), each
+// an Fp2 Karatsuba product of 3 Fp products -> 18 lanes.  Then, with
+// c0_j = u - t - xi t and c1_j = 2 t:
+//   a0' = 3 c0_0 - 2 a0   a2' = 3 c0_1 - 2 a2   a4' = 3 c0_2 - 2 a4
+//   a3' = 3 c1_0 + 2 a3   a5' = 3 c1_1 + 2 a5   a1' = 3 xi c1_2 + 2 a1
+// In parts p (of t) and q (of u):
+//   c0.re = q0 - q1 - 3 p0 + p1 + p2      c0.im = q2 - q0 - q1 + p0 + 3 p1 - 2 p2
+//   c1.re = 2 p0 - 2 p1                   c1.im = 2 p2 - 2 p0 - 2 p1
+//   (xi c1).re = 4 p0 - 2 p2              (xi c1).im = 2 p2 - 4 p1
+template <class C>
+KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
+  const uint32_t* a = vw_smem + a_o;
+  const int lane = threadIdx.x;
+  if (lane < 18) {
+    const int j = lane / 6, which = (lane / 3) & 1;
+    const Fp2<C> x = vw_ld2<C>(a + j * E2), y = vw_ld2<C>(a + (j + 3) * E2);
+    Fp2<C> X = x, Y = y;
+    if (which) {
+      X = f2_add<C>(x, y);
+      Y = f2_add<C>(x, f2_mul_xi<C>(y));
+    }
+    vw_st<C>(prod + lane * L, vw_part<C>(X, Y, lane % 3));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    const int k = lane >> 1, im = lane & 1;
+    const int j = (k & 1) ? (k == 3 ? 0 : k == 5 ? 1 : 2) : (k >> 1);
+    const uint32_t* q = prod + j * 6 * L;
+    int cp0, cp1, cp2, cq0 = 0, cq1 = 0, cq2 = 0;
+    if (!(k & 1)) {
+      cp0 = im ? 1 : -3;
+      cp1 = im ? 3 : 1;
+      cp2 = im ? -2 : 1;
+      cq0 = im ? -1 : 1;
+      cq1 = -1;
+      cq2 = im ? 1 : 0;
+    } else if (k != 1) {
+      cp0 = im ? -2 : 2;
+      cp1 = -2;
+      cp2 = im ? 2 : 0;
+    } else {
+      cp0 = im ? 0 : 4;
+      cp1 = im ? -4 : 0;
+      cp2 = im ? 2 : -2;
+    }
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add<F>(acc, q, cp0);
+    lin_add<F>(acc, q + L, cp1);
+    lin_add<F>(acc, q + 2 * L, cp2);
+    lin_add<F>(acc, q + 3 * L, cq0);
+    lin_add<F>(acc, q + 4 * L, cq1);
+    lin_add<F>(acc, q + 5 * L, cq2);
+    const F29<F> c = lin_fin<F>(acc);
+    lin_init<F>(acc);
+    lin_add<F>(acc, c, 3);
+    lin_add<F>(acc, a + k * E2 + im * L, (k & 1) ? 2 : -2);
+    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+}
+
+template <class C>
+KZGX_DEV void vw_copy(uint32_t dst_o, uint32_t a_o) {
+  uint32_t* dst = vw_smem + dst_o;
+  const uint32_t* a = vw_smem + a_o;
+  for (int w = threadIdx.x; w < VWave<C>::E12; w += 64) dst[w] = a[w];
+  __syncthreads();
+}
+
+template <class C>
+KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o) {
+  uint32_t* dst = vw_smem + dst_o;
+  const uint32_t* a = vw_smem + a_o;
+  using F = typename C::Fp29;
+  constexpr int L = VWave<C>::L;
+  const int lane = threadIdx.x;
+  if (lane < 12) {
+    const int k = lane >> 1;
+    const F29<F> v = vw_ld<C>(a + lane * L);
+    vw_st<C>(dst + lane * L, (k & 1) ? fp_neg<F>(v) : v);
+  }
+  __syncthreads();
+}
+
+template <class C>
+KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o) {
+  uint32_t* dst = vw_smem + dst_o;
+  const uint32_t* a = vw_smem + a_o;
+  using P = typename PairOf<C>::T;
+  constexpr int E2 = VWave<C>::E2;
+  const int k = threadIdx.x;
+  if (k < 6) {
+    Fp2<C> g = f2_const<C>(P::FROB[0]);
+    if (k == 1) g = f2_const<C>(P::FROB[1]);
+    if (k == 2) g = f2_const<C>(P::FROB[2]);
+    if (k == 3) g = f2_const<C>(P::FROB[3]);
+    if (k == 4) g = f2_const<C>(P::FROB[4]);
+    if (k == 5) g = f2_const<C>(P::FROB[5]);
+    vw_st2<C>(dst + k * E2, f2_mul<C>(f2_conj<C>(vw_ld2<C>(a + k * E2)), g));
+  }
+  __syncthreads();
+}
+
+// one lane: the tower inverse
+template <class C>
+KZGX_TW void vw_inv(uint32_t dst_o, uint32_t a_o) {
+  uint32_t* dst = vw_smem + dst_o;
+  const uint32_t* a = vw_smem + a_o;
+  constexpr int E2 = VWave<C>::E2;
+  if (threadIdx.x == 0) {
+    Fp12<C> x;
+    x.c0.c0 = vw_ld2<C>(a + 0 * E2);
+    x.c1.c0 = vw_ld2<C>(a + 1 * E2);
+    x.c0.c1 = vw_ld2<C>(a + 2 * E2);
+    x.c1.c1 = vw_ld2<C>(a + 3 * E2);
+    x.c0.c2 = vw_ld2<C>(a + 4 * E2);
+    x.c1.c2 = vw_ld2<C>(a + 5 * E2);
+    const Fp12<C> r = f12_inv<C>(x);
+    vw_st2<C>(dst + 0 * E2, r.c0.c0);
+    vw_st2<C>(dst + 1 * E2, r.c1.c0);
+    vw_st2<C>(dst + 2 * E2, r.c0.c1);
+    vw_st2<C>(dst + 3 * E2, r.c1.c1);
+    vw_st2<C>(dst + 4 * E2, r.c0.c2);
+    vw_st2<C>(dst + 5 * E2, r.c1.c2);
+  }
+  __syncthreads();
+}
+
+// final exponentiation as a small program over Fp12 slots (the chains of
+// final_exp), run by one loop so that every wave-wide op is inlined once and
+// no call (with its register save / restore through scratch) sits between
+// rounds.  Slots: 0 f, 1 g, 2 t0, 3 t1, 4 a, 5 b, 6 c, 7 t2, 8 t3.
+enum : uint8_t { VW_MUL, VW_CSQR, VW_CONJ, VW_FROB, VW_INV, VW_POWZ, VW_POWS, VW_POWK3 };
+// easy part f^(p^6 - 1)(p^2 + 1) -> g, then the BN254 hard part in u
+__constant__ uint8_t vw_fe_bn[][4] = {
+    {VW_INV, 2, 0, 0},   {VW_CONJ, 1, 0, 0},  {VW_MUL, 1, 1, 2},   {VW_FROB, 2, 1, 0},  {VW_FROB, 2, 2, 0},
+    {VW_MUL, 1, 2, 1},   {VW_POWZ, 4, 1, 0},  {VW_POWZ, 5, 4, 0},  {VW_POWZ, 6, 5, 0},  {VW_POWS, 2, 6, 36},
+    {VW_POWS, 3, 5, 30}, {VW_MUL, 0, 2, 3},   {VW_POWS, 3, 4, 18}, {VW_MUL, 0, 0, 3},   {VW_CSQR, 3, 1, 0},
+    {VW_MUL, 0, 0, 3},   {VW_CONJ, 0, 0, 0},  {VW_POWS, 3, 5, 18}, {VW_POWS, 7, 4, 12}, {VW_MUL, 3, 3, 7},
+    {VW_MUL, 3, 2, 3},   {VW_CONJ, 3, 3, 0},  {VW_MUL, 3, 3, 1},   {VW_POWS, 7, 5, 6},  {VW_MUL, 7, 7, 1},
+    {VW_FROB, 3, 3, 0},  {VW_MUL, 0, 0, 3},   {VW_FROB, 7, 7, 0},  {VW_FROB, 7, 7, 0},  {VW_MUL, 0, 0, 7},
+    {VW_FROB, 8, 1, 0},  {VW_FROB, 8, 8, 0},  {VW_FROB, 8, 8, 0},  {VW_MUL, 0, 0, 8}};
+// easy part, then BLS12: t = g^K3, t2 = t^(x + p), t3 = t2^(x^2 + p^2 - 1), f = t3 g
+__constant__ uint8_t vw_fe_bls[][4] = {
+    {VW_INV, 2, 0, 0},  {VW_CONJ, 1, 0, 0}, {VW_MUL, 1, 1, 2},  {VW_FROB, 2, 1, 0}, {VW_FROB, 2, 2, 0},
+    {VW_MUL, 1, 2, 1},  {VW_POWK3, 2, 1, 0}, {VW_POWZ, 3, 2, 0}, {VW_FROB, 2, 2, 0}, {VW_MUL, 3, 3, 2},
+    {VW_POWZ, 4, 3, 0}, {VW_POWZ, 5, 4, 0}, {VW_FROB, 2, 3, 0}, {VW_FROB, 2, 2, 0}, {VW_MUL, 5, 5, 2},
+    {VW_CONJ, 2, 3, 0}, {VW_MUL, 5, 5, 2},  {VW_MUL, 0, 5, 1}};
+
+template <class C>
+KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
+  using P = typename PairOf<C>::T;
+  constexpr int E = VWave<C>::E12;
+  const int nops = P::IS_BN ? (int)(sizeof(vw_fe_bn) / 4) : (int)(sizeof(vw_fe_bls) / 4);
+  for (int k = 0; k < nops; k++) {
+    const uint8_t* op = P::IS_BN ? vw_fe_bn[k] : vw_fe_bls[k];
+    const uint32_t d = slots + op[1] * E, a = slots + op[2] * E, b = slots + op[3] * E;
+    switch (op[0]) {
+      case VW_MUL: vw_mul<C>(d, a, b, prod); break;
+      case VW_CSQR: vw_cyclo_sqr<C>(d, a, prod); break;
+      case VW_CONJ: vw_conj<C>(d, a); break;
+      case VW_FROB: vw_frob<C>(d, a); break;
+      case VW_INV: vw_inv<C>(d, a); break;
+      default: {  // d = a^e (cyclotomic a, top bit of e set), d != a
+        uint64_t e0 = op[3], e1 = 0;
+        int bits = 32 - __builtin_clz((uint32_t)op[3] | 1u);
+        if (op[0] == VW_POWZ) {
+          e0 = P::Z_ABS;
+          bits = 64 - __builtin_clzll(P::Z_ABS);
+        } else if (op[0] == VW_POWK3) {
+          e0 = P::K3[0];
+          e1 = P::K3[1];
+          bits = P::K3_BITS;
+        }
+        vw_copy<C>(d, a);
+#pragma unroll 1
+        for (int i = bits - 2; i >= 0; i--) {
+          vw_cyclo_sqr<C>(d, d, prod);
+          if (((i < 64 ? e0 >> i : e1 >> (i - 64)) & 1ull)) vw_mul<C>(d, d, a, prod);
+        }
+        if (op[0] == VW_POWZ && P::Z_NEG) vw_conj<C>(d, d);
+      }
+    }
+  }
+}
+
+// multi-Miller loop of both pairings over the shared loop count, one line
+// product site: line s is a doubling line (square first, except at the top
+// bit), an addition line (after a doubling line of a set bit), or (BN) one of
+// the two Frobenius lines after the conjugation
+template <class C>
+KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  constexpr int NLOOP = V::NL - (P::D_TWIST ? 2 : 0);
+  int i = P::LOOP_BITS - 2;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < V::NL; s++) {
+    if (s < NLOOP) {
+      if (add_next) {
+        add_next = false;
+        i--;
+      } else {
+        if (i != P::LOOP_BITS - 2) vw_sqr<C>(f, f, prod);  // f = 1 before the first line
+        add_next = (P::LOOP[i >> 6] >> (i & 63)) & 1ull;
+        if (!add_next) i--;
+      }
+    } else if (s == NLOOP && P::LOOP_NEG) {
+      vw_conj<C>(f, f);
+    }
+#pragma unroll 1
+    for (int q = 0; q < 2; q++)
+      if ((use_mask >> q) & 1) vw_mul_line<C>(f, V::O_LINES + (q * V::NL + s) * V::LW, prod);
+  }
+  if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C>(f, f);
+}
+
+// The same line table for a variable Q with the G2 chain spread over a wave
+// (k_vlines runs it on one lane: ~25 dependent Fp2 operations per step).
+// Each step is a few rounds of independent Fp2 products, one Karatsuba part
+// per lane, folded lazily (LinAcc):
+//   doubling (dbl-2009-l + tangent):  [X^2, Y^2, Z^2, YZ] -> [2YZ ZZ, E ZZ, E X, B^2,
+//                                     (X+B)^2, E^2] -> [E (D - X3)]
+//   addition (madd-2007-bl + chord): [Z^2] -> [qx Z1Z1, Z Z1Z1] -> [qy ZZZ, H^2, Z H]
+//                                     -> [H I, X I, r^2, r qx, qy Z3] -> [Y J, r (V - X3)]
+// Any Jacobian representative gives the lines up to Fp2 factors, which the
+// final exponentiation removes.  T = O or H = 0 (impossible for Q of order
+// r) sets redo[q]; k_vlines_redo then recomputes that table on one lane.
+template <class C>
+struct VLine {
+  static constexpr int L = C::Fp29::L, E2 = 2 * L;
+  // Fp2 slots
+  enum { X, Y, Z, QX, QY, Q1X, Q1Y, Q2X, Q2Y, A, B, ZZ, YZ, D, CC, Z1Z1, U2, ZZZ, H, R, Z3, I, J, V, NS };
+  static constexpr int PROD = NS * E2;  // 18 parts of L words
+  static constexpr int FLAG = PROD + 18 * L;
+  static constexpr int WORDS = FLAG + 4;
+};
+
+template <class C>
+KZGX_DEV uint32_t* vl_slot(int k) {
+  return vw_smem + k * VLine<C>::E2;
+}
+// lanes < 3 n: part (lane % 3) of product lane / 3, operands from `ops`
+template <class C, class Ops>
+KZGX_DEV void vl_parts(int n, Ops ops) {
+  const int lane = threadIdx.x;
+  if (lane < 3 * n) {
+    Fp2<C> x, y;
+    ops(lane / 3, x, y);
+    vw_st<C>(vw_smem + VLine<C>::PROD + lane * VLine<C>::L, vw_part<C>(x, y, lane % 3));
+  }
+  __syncthreads();
+}
+template <class C>
+KZGX_DEV const uint32_t* vl_prod(int k) {
+  return vw_smem + VLine<C>::PROD + 3 * k * VLine<C>::L;
+}
+template <class C>
+KZGX_DEV const uint32_t* vl_comp(int slot, int im) {
+  return vw_smem + slot * VLine<C>::E2 + im * VLine<C>::L;
+}
+
+template <class C>
+KZGX_DEV void vl_dbl_wave(uint32_t* out) {
+  using F = typename C::Fp29;
+  using S = VLine<C>;
+  constexpr int L = S::L, E2 = S::E2;
+  const int lane = threadIdx.x;
+  // round 1: A = X^2, B = Y^2, ZZ = Z^2, YZ = Y Z
+  vl_parts<C>(4, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const int a = k == 0 ? S::X : k == 1 ? S::Y : k == 2 ? S::Z : S::Y;
+    const int b = k == 3 ? S::Z : a;
+    x = vw_ld2<C>(vl_slot<C>(a));
+    y = vw_ld2<C>(vl_slot<C>(b));
+  });
+  if (lane < 8) {
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(k), im, false, 1);
+    const int dst = k == 0 ? S::A : k == 1 ? S::B : k == 2 ? S::ZZ : S::YZ;
+    vw_st<C>(vl_slot<C>(dst) + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  // round 2: 2YZ ZZ, E ZZ, E X, B^2, (X + B)^2, E^2 with E = 3A
+  vl_parts<C>(6, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+    const Fp2<C> E = f2_add<C>(f2_dbl<C>(a), a);
+    if (k == 0) {
+      x = f2_dbl<C>(vw_ld2<C>(vl_slot<C>(S::YZ)));
+      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+    } else if (k == 1) {
+      x = E;
+      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+    } else if (k == 2) {
+      x = E;
+      y = vw_ld2<C>(vl_slot<C>(S::X));
+    } else if (k == 3) {
+      x = y = vw_ld2<C>(vl_slot<C>(S::B));
+    } else if (k == 4) {
+      x = y = f2_add<C>(vw_ld2<C>(vl_slot<C>(S::X)), vw_ld2<C>(vl_slot<C>(S::B)));
+    } else {
+      x = y = E;
+    }
+  });
+  // w0c = P0, w1c = -P1, w3c = P2 - 2B, C = P3, D = 2 P4 - 2A - 2 P3,
+  // X3 = P5 - 2D = P5 - 4 P4 + 4A + 4 P3, Z3 = 2 YZ
+  if (lane < 14) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    switch (w) {
+      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -1); break;
+      case 2:
+        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
+        lin_add<F>(acc, vl_comp<C>(S::B, im), -2);
+        break;
+      case 3: lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1); break;
+      case 4:
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, 2);
+        lin_add<F>(acc, vl_comp<C>(S::A, im), -2);
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, -2);
+        break;
+      case 5:
+        lin_add_f2<F>(acc, vl_prod<C>(5), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -4);
+        lin_add<F>(acc, vl_comp<C>(S::A, im), 4);
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 4);
+        break;
+      default: lin_add<F>(acc, vl_comp<C>(S::YZ, im), 2); break;
+    }
+    const F29<F> v = lin_fin_wide<F>(acc);
+    if (w < 3) {
+      vw_st<C>(out + w * E2 + im * L, v);
+    } else {
+      const int dst = w == 3 ? S::CC : w == 4 ? S::D : w == 5 ? S::X : S::Z;
+      vw_st<C>(vl_slot<C>(dst) + im * L, v);
+    }
+  }
+  __syncthreads();
+  // round 3: Y3 = E (D - X3) - 8 C
+  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+    x = f2_add<C>(f2_dbl<C>(a), a);
+    y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::D)), vw_ld2<C>(vl_slot<C>(S::X)));
+  });
+  if (lane < 2) {
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(0), lane, false, 1);
+    lin_add<F>(acc, vl_comp<C>(S::CC, lane), -8);
+    vw_st<C>(vl_slot<C>(S::Y) + lane * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::Z)))) vw_smem[S::FLAG] = 1u;  // T = O
+  __syncthreads();
+}
+
+// T += q (q = slots qx, qy) and the chord line into out
+template <class C>
+KZGX_DEV void vl_add_wave(int qx, int qy, uint32_t* out) {
+  using F = typename C::Fp29;
+  using S = VLine<C>;
+  constexpr int L = S::L, E2 = S::E2;
+  const int lane = threadIdx.x;
+  auto fin1 = [&](int k, int dst, int d) {  // lanes 2k, 2k+1: slot dst = d * product k
+    if ((lane >> 1) == k) {
+      LinAcc<F> acc;
+      lin_init<F>(acc);
+      lin_add_f2<F>(acc, vl_prod<C>(k), lane & 1, false, d);
+      vw_st<C>(vl_slot<C>(dst) + (lane & 1) * L, lin_fin<F>(acc));
+    }
+  };
+  // Z1Z1 = Z^2
+  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) { x = y = vw_ld2<C>(vl_slot<C>(S::Z)); });
+  fin1(0, S::Z1Z1, 1);
+  __syncthreads();
+  // U2 = qx Z1Z1, ZZZ = Z Z1Z1
+  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qx : S::Z));
+    y = vw_ld2<C>(vl_slot<C>(S::Z1Z1));
+  });
+  fin1(0, S::U2, 1);
+  fin1(1, S::ZZZ, 1);
+  __syncthreads();
+  if (lane < 2) {  // H = U2 - X
+    const int im = lane;
+    vw_st<C>(vl_slot<C>(S::H) + im * L, fp_sub<F>(vw_ld<C>(vl_comp<C>(S::U2, im)), vw_ld<C>(vl_comp<C>(S::X, im))));
+  }
+  __syncthreads();
+  // S2 = qy ZZZ, HH = H^2, ZH = Z H
+  vl_parts<C>(3, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qy : k == 1 ? S::H : S::Z));
+    y = vw_ld2<C>(vl_slot<C>(k == 0 ? S::ZZZ : S::H));
+  });
+  // r = 2 (S2 - Y), I = 4 HH, Z3 = 2 ZH
+  if (lane < 6) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, vl_prod<C>(w), im, false, w == 1 ? 4 : 2);
+    if (w == 0) lin_add<F>(acc, vl_comp<C>(S::Y, im), -2);
+    vw_st<C>(vl_slot<C>(w == 0 ? S::R : w == 1 ? S::I : S::Z3) + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::H)))) vw_smem[S::FLAG] = 1u;  // T = +-q
+  // J = H I, V = X I, r^2, r qx, qy Z3
+  vl_parts<C>(5, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const int a = k == 0 ? S::H : k == 1 ? S::X : k == 4 ? qy : S::R;
+    const int b = k <= 1 ? S::I : k == 2 ? S::R : k == 3 ? qx : S::Z3;
+    x = vw_ld2<C>(vl_slot<C>(a));
+    y = vw_ld2<C>(vl_slot<C>(b));
+  });
+  // J, V; X3 = r^2 - J - 2V; line: w0c = Z3, w1c = -r, w3c = r qx - qy Z3
+  if (lane < 12) {
+    const int w = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    switch (w) {
+      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, 1); break;
+      case 2:
+        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(0), im, false, -1);
+        lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+        break;
+      case 3: lin_add<F>(acc, vl_comp<C>(S::Z3, im), 1); break;
+      case 4: lin_add<F>(acc, vl_comp<C>(S::R, im), -1); break;
+      default:
+        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -1);
+        break;
+    }
+    const F29<F> v = lin_fin<F>(acc);
+    if (w < 3)
+      vw_st<C>(vl_slot<C>(w == 0 ? S::J : w == 1 ? S::V : S::D) + im * L, v);  // D holds X3 for now
+    else
+      vw_st<C>(out + (w - 3) * E2 + im * L, v);
+  }
+  __syncthreads();
+  // Y3 = r (V - X3) - 2 Y J
+  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    if (k == 0) {
+      x = vw_ld2<C>(vl_slot<C>(S::R));
+      y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::V)), vw_ld2<C>(vl_slot<C>(S::D)));
+    } else {
+      x = vw_ld2<C>(vl_slot<C>(S::Y));
+      y = vw_ld2<C>(vl_slot<C>(S::J));
+    }
+  });
+  if (lane < 6) {  // new T: X = X3, Y = Y3, Z = Z3
+    const int w = lane >> 1, im = lane & 1;
+    F29<F> v;
+    if (w == 0) {
+      v = vw_ld<C>(vl_comp<C>(S::D, im));
+    } else if (w == 1) {
+      LinAcc<F> acc;
+      lin_init<F>(acc);
+      lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1);
+      lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+      v = lin_fin<F>(acc);
+    } else {
+      v = vw_ld<C>(vl_comp<C>(S::Z3, im));
+    }
+    vw_st<C>(vl_slot<C>(w) + im * L, v);  // slots X, Y, Z are 0, 1, 2
+  }
+  __syncthreads();
+}
+
+// block q: the line table of Q_q (canonical) into lines + q NL LW
+template <class C>
+__global__ __launch_bounds__(64) void k_vlines_wave(const uint32_t* __restrict__ g2, uint32_t* __restrict__ lines,
+                                                    uint32_t* __restrict__ qfin, uint32_t* __restrict__ redo) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  using S = VLine<C>;
+  const int q = blockIdx.x;
+  uint32_t* out = lines + (size_t)q * V::NL * V::LW;
+  if (threadIdx.x == 0) {
+    G2A<C> Q;
+    const bool fin = g2_from_canon<C>(g2 + q * 4 * C::Fp::N, Q);
+    qfin[q] = fin ? 1u : 0u;
+    redo[q] = 0u;
+    vw_smem[S::FLAG] = fin ? 0u : 2u;
+    vw_st2<C>(vl_slot<C>(S::X), Q.x);
+    vw_st2<C>(vl_slot<C>(S::Y), Q.y);
+    vw_st2<C>(vl_slot<C>(S::Z), f2_one<C>());
+    vw_st2<C>(vl_slot<C>(S::QX), Q.x);
+    vw_st2<C>(vl_slot<C>(S::QY), Q.y);
+    if (P::D_TWIST) {
+      const G2A<C> q1 = twist_frob<C>(Q);
+      G2A<C> q2 = twist_frob<C>(q1);
+      q2.y = f2_neg<C>(q2.y);
+      vw_st2<C>(vl_slot<C>(S::Q1X), q1.x);
+      vw_st2<C>(vl_slot<C>(S::Q1Y), q1.y);
+      vw_st2<C>(vl_slot<C>(S::Q2X), q2.x);
+      vw_st2<C>(vl_slot<C>(S::Q2Y), q2.y);
+    }
+  }
+  __syncthreads();
+  if (vw_smem[S::FLAG] == 2u) return;  // Q = O: no table (uniform)
+  int s = 0;
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    vl_dbl_wave<C>(out + (s++) * V::LW);
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) vl_add_wave<C>(S::QX, S::QY, out + (s++) * V::LW);
+  }
+  if (P::LOOP_NEG && threadIdx.x < 2) {
+    using F = typename C::Fp29;
+    uint32_t* y = vl_slot<C>(S::Y) + threadIdx.x * S::L;
+    vw_st<C>(y, fp_neg<F>(vw_ld<C>(y)));
+  }
+  __syncthreads();
+  if (P::D_TWIST) {
+    vl_add_wave<C>(S::Q1X, S::Q1Y, out + (s++) * V::LW);
+    vl_add_wave<C>(S::Q2X, S::Q2Y, out + (s++) * V::LW);
+  }
+  if (threadIdx.x == 0 && vw_smem[S::FLAG]) redo[q] = 1u;
+}
+
+// single-lane recompute of the tables flagged by k_vlines_wave
+template <class C>
+__global__ __launch_bounds__(64) void k_vlines_redo(const uint32_t* __restrict__ g2, uint32_t* __restrict__ lines,
+                                                    const uint32_t* __restrict__ redo) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  const int q = threadIdx.x;
+  if (q >= 2 || !redo[q]) return;
+  G2A<C> Q;
+  (void)g2_from_canon<C>(g2 + q * 4 * C::Fp::N, Q);
+  uint32_t* out = lines + (size_t)q * V::NL * V::LW;
+  int s = 0;
+  G2J<C> T = g2_from_affine<C>(Q);
+  for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+    vl_dbl<C>(T, out + (s++) * V::LW);
+    if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) vl_add<C>(T, Q, out + (s++) * V::LW);
+  }
+  if (P::LOOP_NEG) T.Y = f2_neg<C>(T.Y);
+  if (P::D_TWIST) {
+    const G2A<C> q1 = twist_frob<C>(Q);
+    G2A<C> q2 = twist_frob<C>(q1);
+    q2.y = f2_neg<C>(q2.y);
+    vl_add<C>(T, q1, out + (s++) * V::LW);
+    vl_add<C>(T, q2, out + (s++) * V::LW);
+  }
+}
+
+// the product of the two pairings (P_q, Q_q), q = 0, 1, from the line tables
+// of Q_0, Q_1 (k_vlines) and the per-pairing scale factors and use flags the
+// caller left in LDS (scale: [q][yP, xP, 1] up to an Fp factor; flag[q]);
+// *ok_out = (product after the final exponentiation == 1)
+template <class C>
+KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __restrict__ ok_out) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int L = V::L, E2 = V::E2;
+  uint32_t* lines = vw_smem + V::O_LINES;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  const int lane = threadIdx.x;
+  const bool use0 = flag[0] != 0, use1 = flag[1] != 0;
+  // ---- scale the precomputed lines
+  for (int t = lane; t < 2 * V::NL * 3; t += 64) {
+    const int q = t / (3 * V::NL), c = t % 3;
+    const uint32_t* src = vlines + (size_t)t * E2;  // [q][s][c] order matches t
+    vw_st2<C>(lines + t * E2, f2_mul_fp<C>(vw_ld2<C>(src), vw_ld<C>(scale + (q * 3 + c) * L)));
+  }
+  // f = 1
+  constexpr uint32_t f = V::O_SLOT, pr = V::O_PROD;
+  if (lane < 12) vw_st<C>(vw_smem + f + lane * L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  __syncthreads();
+  VW_STAMP(3);
+  vw_miller<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr);
+  VW_STAMP(4);
+  vw_final_exp<C>(V::O_SLOT, pr);
+  VW_STAMP(8);
+  // ---- f == 1 ?
+  if (lane < 12) {
+    const F29<F> v = f29_reduce<F>(vw_ld<C>(vw_smem + f + lane * L));
+    const F29<F> want = lane == 0 ? f29_reduce<F>(f29_one<F>()) : f29_zero<F>();
+    uint32_t diff = 0;
+    for (int i = 0; i < L; i++) diff |= v.v[i] ^ want.v[i];
+    flag[2 + lane] = diff;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t bad = 0;
+    for (int i = 0; i < 12; i++) bad |= flag[2 + i];
+    *ok_out = bad == 0 ? 1u : 0u;
+#ifdef KZGX_VW_TIMING
+    if (blockIdx.x == 0)
+      printf("vw_ts tree %llu d %llu scale %llu miller %llu final_exp %llu (x10ns)\n", vw_ts[1] - vw_ts[0],
+             vw_ts[2] - vw_ts[1], vw_ts[3] - vw_ts[2], vw_ts[4] - vw_ts[3], vw_ts[8] - vw_ts[4]);
+#endif
+  }
+}
+
+// block (one wave) per opening; same contract as k_verify_single
+template <class C>
+__global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__ commits,
+                                                    const uint32_t* __restrict__ commit_inf,
+                                                    const uint32_t* __restrict__ proofs,
+                                                    const uint32_t* __restrict__ proof_inf,
+                                                    const uint32_t* __restrict__ zs, const uint32_t* __restrict__ ys,
+                                                    uint32_t count, const uint32_t* __restrict__ g1_0,
+                                                    const uint32_t* __restrict__ vtab, const uint32_t* __restrict__ vlines,
+                                                    const uint32_t* __restrict__ qfin, uint32_t* __restrict__ ok) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int N = C::Fp::N, L = V::L;
+  uint32_t* prod = vw_smem + V::O_PROD;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  const uint32_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (k >= count) return;  // uniform over the block
+  VW_STAMP(0);
+  // ---- [y]G: lane w takes window w's table entry, then a 5-level tree
+  Affine<C> g;
+  const bool gf = affine_from_canonical<C>(g1_0, g);
+  if (lane < 32) {
+    const uint32_t d = (ys[(size_t)k * 8 + (lane >> 2)] >> (8 * (lane & 3))) & 255u;
+    Xyzz<C> p = xyzz_inf<C>();
+    if (gf && d) p = xyzz_from_affine<C>(affine_load<C>(vtab + ((size_t)lane * 255 + d - 1) * V::AW));
+    xyzz_store<C>(prod + lane * 4 * L, p);
+  }
+  __syncthreads();
+  for (int s = 16; s >= 1; s >>= 1) {
+    if (lane < s)
+      xyzz_store<C>(prod + lane * 4 * L,
+                    xyzz_add<C>(xyzz_load<C>(prod + lane * 4 * L), xyzz_load<C>(prod + (lane + s) * 4 * L)));
+    __syncthreads();
+  }
+  VW_STAMP(1);
+  // ---- D = C - [y]G + [z]pi and the per-pairing scale factors (lane 0)
+  if (lane == 0) {
+    Affine<C> c, pi;
+    const bool cf = affine_from_canonical<C>(commits + (size_t)k * 2 * N, c) && !(commit_inf && commit_inf[k]);
+    const bool pf = affine_from_canonical<C>(proofs + (size_t)k * 2 * N, pi) && !(proof_inf && proof_inf[k]);
+    Xyzz<C> d = xyzz_neg<C>(xyzz_load<C>(prod));
+    if (cf) d = xyzz_add_affine<C>(d, c);
+    if (pf) {
+      int top = -1;
+      for (int b = 255; b >= 0 && top < 0; b--)
+        if ((zs[(size_t)k * 8 + (b >> 5)] >> (b & 31)) & 1u) top = b;
+      Xyzz<C> zp = xyzz_inf<C>();
+      for (int b = top; b >= 0; b--) {
+        zp = xyzz_dbl<C>(zp);
+        if ((zs[(size_t)k * 8 + (b >> 5)] >> (b & 31)) & 1u) zp = xyzz_add_affine<C>(zp, pi);
+      }
+      d = xyzz_add<C>(d, zp);
+    }
+    const bool df = !xyzz_is_inf<C>(d);
+    // pairing 0: (-D, G2[0]) with line factors (-Y ZZ, X ZZZ, ZZ ZZZ)
+    vw_st<C>(scale + 0 * L, fp_neg<F>(f29_mul<F>(d.Y, d.ZZ)));
+    vw_st<C>(scale + 1 * L, f29_mul<F>(d.X, d.ZZZ));
+    vw_st<C>(scale + 2 * L, f29_mul<F>(d.ZZ, d.ZZZ));
+    // pairing 1: (pi, G2[1]) with (y, x, 1)
+    vw_st<C>(scale + 3 * L, pi.y);
+    vw_st<C>(scale + 4 * L, pi.x);
+    vw_st<C>(scale + 5 * L, f29_one<F>());
+    flag[0] = (df && qfin[0]) ? 1u : 0u;
+    flag[1] = (pf && qfin[1]) ? 1u : 0u;
+  }
+  __syncthreads();
+  VW_STAMP(2);
+  vw_pair_tail<C>(vlines, ok + k);
+}
+
+// one wave: e(P_0, Q_0) e(-P_1, Q_1) == 1 for canonical affine G1 points
+// p = (P_0, P_1) and the line tables of (Q_0, Q_1); the pairing-equation form
+// of verify_proof with more than one point (e(pi, [Z(tau)]G2) ==
+// e(C - [I(tau)]G1, G2[0]))
+template <class C>
+__global__ __launch_bounds__(64) void k_pair2_wave(const uint32_t* __restrict__ p, const uint32_t* __restrict__ p_inf,
+                                                   const uint32_t* __restrict__ q_inf,
+                                                   const uint32_t* __restrict__ vlines,
+                                                   const uint32_t* __restrict__ qfin, uint32_t* __restrict__ ok) {
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  constexpr int N = C::Fp::N, L = V::L;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 2; q++) {
+      Affine<C> a;
+      const bool fin = affine_from_canonical<C>(p + q * 2 * N, a) && !(p_inf && p_inf[q]);
+      vw_st<C>(scale + (q * 3 + 0) * L, q ? fp_neg<F>(a.y) : a.y);
+      vw_st<C>(scale + (q * 3 + 1) * L, a.x);
+      vw_st<C>(scale + (q * 3 + 2) * L, f29_one<F>());
+      flag[q] = (fin && qfin[q] && !(q_inf && q_inf[q])) ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  vw_pair_tail<C>(vlines, ok);
+}
+
+// wave path: [y]G table | line tables | Q flags, in one device buffer
+template <class C>
+static constexpr size_t vw_tab_words() {
+  return (size_t)VWave<C>::TAB * VWave<C>::AW;
+}
+template <class C>
+static constexpr size_t vw_buf_words() {
+  return vw_tab_words<C>() + (size_t)2 * VWave<C>::NL * VWave<C>::LW + 4;
+}
+
+size_t verify_wave_bytes(int curve) {
+  return 4 * (curve == KZGX_CURVE_BN254 ? vw_buf_words<BN254G1>() : vw_buf_words<BLS12381G1>());
+}
+
+template <class C>
+static int verify_wave_prepare_impl(const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st) {
+  uint32_t* lines = d_buf + vw_tab_words<C>();
+  uint32_t* qfin = lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
+  hipLaunchKernelGGL(k_vtab<C>, dim3((VWave<C>::TAB + 63) / 64), dim3(64), 0, st, d_g1_0, d_buf);
+  hipLaunchKernelGGL(k_vlines<C>, dim3(1), dim3(64), 0, st, d_g2_01, lines, qfin);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st) {
+  ProfScope p(ctx, st, "verify_wave_prepare");
+  return ctx->curve == KZGX_CURVE_BN254 ? verify_wave_prepare_impl<BN254G1>(d_g1_0, d_g2_01, d_buf, st)
+                                        : verify_wave_prepare_impl<BLS12381G1>(d_g1_0, d_g2_01, d_buf, st);
+}
+
+template <class C>
+static int verify_wave_impl(const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
+                            const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
+                            const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st) {
+  const uint32_t* lines = d_buf + vw_tab_words<C>();
+  const uint32_t* qfin = lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
+  hipLaunchKernelGGL(k_verify_wave<C>, dim3((unsigned)count), dim3(64), VWave<C>::WORDS * 4, st, d_commits, d_commit_inf, d_proofs,
+                     d_proof_inf, d_z, d_y, (uint32_t)count, d_g1_0, d_buf, lines, qfin, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
+                      const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
+                      const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st) {
+  if (count == 0) return KZGX_OK;
+  ProfScope p(ctx, st, "verify_wave");
+  return ctx->curve == KZGX_CURVE_BN254
+             ? verify_wave_impl<BN254G1>(d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y, count, d_g1_0,
+                                         d_buf, d_ok, st)
+             : verify_wave_impl<BLS12381G1>(d_commits, d_commit_inf, d_proofs, d_proof_inf, d_z, d_y, count, d_g1_0,
+                                            d_buf, d_ok, st);
+}
+
+template <class C>
+static int pair2_wave_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+                           uint32_t* d_lines, uint32_t* d_ok, hipStream_t st) {
+  uint32_t* qfin = d_lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
+  hipLaunchKernelGGL(k_vlines_wave<C>, dim3(2), dim3(64), VLine<C>::WORDS * 4, st, d_q, d_lines, qfin, qfin + 2);
+  hipLaunchKernelGGL(k_vlines_redo<C>, dim3(1), dim3(64), 0, st, d_q, d_lines, qfin + 2);
+  hipLaunchKernelGGL(k_pair2_wave<C>, dim3(1), dim3(64), VWave<C>::WORDS * 4, st, d_p, d_p_inf, d_q_inf, d_lines,
+                     qfin, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+size_t pair2_wave_scratch_bytes(int curve) {
+  return 4 * (curve == KZGX_CURVE_BN254 ? (size_t)2 * VWave<BN254G1>::NL * VWave<BN254G1>::LW + 4
+                                        : (size_t)2 * VWave<BLS12381G1>::NL * VWave<BLS12381G1>::LW + 4);
+}
+
+int pair2_wave(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+               uint32_t* d_scratch, uint32_t* d_ok, hipStream_t st) {
+  ProfScope p(ctx, st, "pair2_wave");
+  return ctx->curve == KZGX_CURVE_BN254 ? pair2_wave_impl<BN254G1>(d_p, d_p_inf, d_q, d_q_inf, d_scratch, d_ok, st)
+                                        : pair2_wave_impl<BLS12381G1>(d_p, d_p_inf, d_q, d_q_inf, d_scratch, d_ok, st);
+}
+
+}  // namespace kzgx
