@@ -533,7 +533,8 @@ const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
   ctx->g2tab_n = 0;
   if (kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_g2tab, kzgx::g2_table_bytes(ctx->c.curve, all), &ctx->g2tab_b) !=
           KZGX_OK ||
-      kzgx::g2_table_build(&ctx->c, ctx->d_srs2_canon, all, ctx->d_g2tab, st) != KZGX_OK)
+      kzgx::g2_table_build(&ctx->c, ctx->d_srs2_canon, all, ctx->d_g2tab, st) != KZGX_OK ||
+      hipStreamSynchronize(st) != hipSuccess)
     return nullptr;
   ctx->g2tab_n = all;
   return ctx->d_g2tab;
@@ -714,6 +715,7 @@ int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const 
     if (!ctx->vw_ready) {
       KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
       KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, ctx->d_vw, st));
+      KZGX_TRY_HIP(hipStreamSynchronize(st));  // one-time; later calls may come on other streams
       ctx->vw_ready = true;
     }
     return kzgx::verify_wave_batch(&ctx->c, (const uint32_t*)d_commits, (const uint32_t*)d_commit_inf,
