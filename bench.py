@@ -40,8 +40,8 @@ REF_PROOF_S = 1.080747
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0,
                     help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default 1024, cfg3 4096 "
                          "(BASELINE configs[2]: 4096 openings)")
