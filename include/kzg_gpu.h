@@ -153,6 +153,17 @@ int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z
 int kzgx_g1_validate(kzgx_ctx* ctx, const uint64_t* xy, int* ok);
 /* out = sum of count affine points (is_inf may be NULL); host pointers */
 int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy, int* out_is_inf);
+/* One commitment sharded over several contexts, typically one per GPU (the
+ * one-process form of SURVEY 8e's sharded commit; bench.py's configs[4] runs
+ * the one-process-per-GPU form over RCCL).  Context k holds the SRS slice
+ * starting at point starts[k] (kzgx_gen_srs_g1(ctx, tau, starts[k], n_k) or
+ * kzgx_load_srs_g1); the slices must be contiguous from 0 (starts[k + 1] ==
+ * starts[k] + |SRS_k|, else KZGX_ERR_ARG) and cover n (else
+ * KZGX_ERR_DEGREE).  Every context runs the partial MSM of its slice of
+ * scalars[0..n) on its own stream, concurrently; the partial points are then
+ * folded exactly on ctxs[0] (affine result, bit-exact with one MSM). */
+int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
+                        size_t n, uint64_t* out_xy, int* out_is_inf);
 
 /* ---- verify half: G2 setup, polyeval_G2, pairing ----------------------------
  * G2 points are canonical affine on the sextic twist (BN254: D-type

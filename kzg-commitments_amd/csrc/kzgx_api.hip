@@ -523,6 +523,48 @@ int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t cou
   return KZGX_OK;
 }
 
+int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
+                        size_t n, uint64_t* out_xy, int* out_is_inf) {
+  if (!ctxs || !starts || nctx == 0 || (n > 0 && !scalars) || !out_xy || !out_is_inf) return KZGX_ERR_ARG;
+  std::vector<size_t> cnt(nctx, 0);
+  for (size_t k = 0; k < nctx; k++) {
+    kzgx_ctx* c = ctxs[k];
+    if (!c || c->c.curve != ctxs[0]->c.curve) return KZGX_ERR_ARG;
+    if (c->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+    if (starts[k] != (k == 0 ? 0 : starts[k - 1] + ctxs[k - 1]->c.n_srs)) return KZGX_ERR_ARG;  // contiguous
+    cnt[k] = starts[k] >= n ? 0 : std::min(n - starts[k], c->c.n_srs);
+  }
+  if (starts[nctx - 1] + ctxs[nctx - 1]->c.n_srs < n) return KZGX_ERR_DEGREE;
+  const size_t pb = point_words(ctxs[0]) * 4;
+  std::vector<void*> outs(nctx, nullptr);
+  // every shard's partial MSM, enqueued on its own context's stream
+  for (size_t k = 0; k < nctx; k++) {
+    if (!cnt[k]) continue;
+    kzgx_ctx* c = ctxs[k];
+    KZGX_TRY(activate(c));
+    void* d_s;
+    KZGX_TRY(stage(c, 0, cnt[k] * 32, &d_s));
+    KZGX_TRY(stage(c, 1, pb + 16, &outs[k]));
+    KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars + starts[k] * 4, cnt[k] * 32, hipMemcpyHostToDevice, c->c.stream));
+    KZGX_TRY(kzgx::msm_batch(&c->c, (const uint32_t*)d_s, cnt[k], 1, cnt[k] * 8, (uint32_t*)outs[k],
+                             (uint32_t*)((char*)outs[k] + pb), c->c.stream));
+  }
+  // gather the partial points, then one exact fold on ctxs[0]
+  std::vector<uint64_t> pts(nctx * pb / 8, 0);
+  std::vector<int> infs(nctx, 1);
+  for (size_t k = 0; k < nctx; k++) {
+    if (!cnt[k]) continue;
+    kzgx_ctx* c = ctxs[k];
+    KZGX_TRY(activate(c));
+    uint32_t oi = 1;
+    KZGX_TRY_HIP(hipMemcpyAsync(pts.data() + k * pb / 8, outs[k], pb, hipMemcpyDeviceToHost, c->c.stream));
+    KZGX_TRY_HIP(hipMemcpyAsync(&oi, (char*)outs[k] + pb, 4, hipMemcpyDeviceToHost, c->c.stream));
+    KZGX_TRY_HIP(hipStreamSynchronize(c->c.stream));
+    infs[k] = (int)oi;
+  }
+  return kzgx_g1_sum(ctxs[0], pts.data(), infs.data(), nctx, out_xy, out_is_inf);
+}
+
 /* ---- verify half: G2 SRS, polyeval_G2, pairing, verify_proof ---------------- */
 namespace {
 // the G2 SRS's windowed table for n points (rebuilt when the SRS changed or

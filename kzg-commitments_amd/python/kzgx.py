@@ -28,7 +28,7 @@ EXPORTS = [
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
-    "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max",
+    "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max", "kzgx_msm_g1_sharded",
 ]
 
 _lib = None
@@ -93,6 +93,7 @@ def lib():
             "kzgx_verify_single_batch": (ctypes.c_int, [vp, u64p, intp, u64p, intp, u64p, u64p, sz, intp]),
             "kzgx_verify_single_batch_device": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, sz, vp, vp]),
             "kzgx_set_verify_wave_max": (ctypes.c_int, [vp, sz]),
+            "kzgx_msm_g1_sharded": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(sz), sz, u64p, sz, u64p, intp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -113,6 +114,20 @@ def _chk(rc, where):
 
 def as_scalars(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+
+
+def msm_g1_sharded(ctxs, starts, scalars):
+    """kzgx_msm_g1_sharded: one commitment over contexts holding contiguous SRS
+    slices (context k's slice starts at point starts[k]); -> (xy, is_inf)"""
+    sc = as_scalars(scalars)
+    n = sc.shape[0]
+    hs = (vp * len(ctxs))(*[c.h for c in ctxs])
+    st = (sz * len(ctxs))(*starts)
+    out = np.zeros(2 * ctxs[0].w64, dtype=np.uint64)
+    oi = ctypes.c_int(0)
+    _chk(lib().kzgx_msm_g1_sharded(hs, st, len(ctxs), _p(sc) if n else None, n, _p(out), ctypes.byref(oi)),
+         "kzgx_msm_g1_sharded")
+    return out, bool(oi.value)
 
 
 class Context:
