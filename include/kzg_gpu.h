@@ -123,6 +123,11 @@ int kzgx_msm_g1_batch_device(kzgx_ctx* ctx, const void* d_scalars, size_t n, siz
 int kzgx_quotient_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
                                       const void* d_z, size_t batch, void* d_q, size_t q_stride, void* d_y,
                                       void* stream);
+/* the same with host pointers (the q = (P - I) / Z step of create_proof,
+ * trusted_setup.cpp:225, batched): q_out holds batch x (n - 1) scalars,
+ * y_out (may be NULL) batch scalars; coeff_stride in scalars (0: shared P) */
+int kzgx_quotient_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
+                               const uint64_t* zs, size_t batch, uint64_t* q_out, uint64_t* y_out);
 /* quotient + MSM per opening; host pointers.  out_y may be NULL. */
 int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
                             const uint64_t* zs, size_t batch, uint64_t* out_xy, int* out_is_inf, uint64_t* out_y);

@@ -348,6 +348,30 @@ int kzgx_quotient_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_
                                (uint32_t*)d_q, q_stride * 8, (uint32_t*)d_y, pick(ctx, stream));
 }
 
+int kzgx_quotient_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, size_t coeff_stride,
+                               const uint64_t* zs, size_t batch, uint64_t* q_out, uint64_t* y_out) {
+  KZGX_TRY(activate(ctx));
+  if (batch == 0) return KZGX_OK;
+  if (!zs || (n > 0 && !coeffs) || (n > 1 && !q_out) || n > 0xffffffffu) return KZGX_ERR_ARG;
+  if (batch > 1 && coeff_stride != 0 && coeff_stride < n) return KZGX_ERR_ARG;
+  const size_t nc = coeff_stride == 0 ? n : (batch - 1) * coeff_stride + n;  // coefficient rows read
+  const size_t nq = n > 1 ? n - 1 : 0;
+  void *d_c = nullptr, *d_z, *d_q = nullptr, *d_y;
+  if (nc) KZGX_TRY(stage(ctx, 0, nc * 32, &d_c));
+  KZGX_TRY(stage(ctx, 1, batch * 32, &d_z));
+  if (nq) KZGX_TRY(stage(ctx, 2, batch * nq * 32, &d_q));
+  KZGX_TRY(stage(ctx, 3, batch * 32, &d_y));
+  hipStream_t st = ctx->c.stream;
+  if (nc) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, nc * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_z, zs, batch * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY(kzgx::quotient_single(&ctx->c, (const uint32_t*)d_c, n, coeff_stride * 8, (const uint32_t*)d_z, batch,
+                                 (uint32_t*)d_q, nq * 8, (uint32_t*)d_y, st));
+  if (nq) KZGX_TRY_HIP(hipMemcpyAsync(q_out, d_q, batch * nq * 32, hipMemcpyDeviceToHost, st));
+  if (y_out) KZGX_TRY_HIP(hipMemcpyAsync(y_out, d_y, batch * 32, hipMemcpyDeviceToHost, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  return KZGX_OK;
+}
+
 int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n, size_t coeff_stride,
                                    const void* d_z, size_t batch, void* d_out_xy, void* d_out_is_inf, void* d_y,
                                    void* stream) {

@@ -29,6 +29,7 @@ EXPORTS = [
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
     "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max", "kzgx_msm_g1_sharded",
+    "kzgx_quotient_single_batch",
 ]
 
 _lib = None
@@ -93,6 +94,7 @@ def lib():
             "kzgx_verify_single_batch": (ctypes.c_int, [vp, u64p, intp, u64p, intp, u64p, u64p, sz, intp]),
             "kzgx_verify_single_batch_device": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, sz, vp, vp]),
             "kzgx_set_verify_wave_max": (ctypes.c_int, [vp, sz]),
+            "kzgx_quotient_single_batch": (ctypes.c_int, [vp, u64p, sz, sz, u64p, sz, u64p, u64p]),
             "kzgx_msm_g1_sharded": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(sz), sz, u64p, sz, u64p, intp]),
         }
         for name, (res, args) in sig.items():
@@ -225,6 +227,20 @@ class Context:
         sc = as_scalars(scalars)
         out, inf = self.msm_batch(sc, sc.shape[0], 1)
         return out[0], bool(inf[0])
+
+    def quotient_single_batch(self, coeffs, zs, shared: bool = True):
+        """q_j = (P_j - P_j(z_j)) / (X - z_j) and y_j = P_j(z_j) (host buffers);
+        coeffs: n x 4 (shared) or batch x n x 4 words -> (q: batch x (n-1) x 4, y: batch x 4)"""
+        c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+        z = as_scalars(zs)
+        batch = z.shape[0]
+        n = c.shape[-2] if c.ndim == 3 else c.reshape(-1, 4).shape[0]
+        stride = 0 if shared else n
+        q = np.zeros((batch, max(n - 1, 0), 4), dtype=np.uint64)
+        y = np.zeros((batch, 4), dtype=np.uint64)
+        _chk(lib().kzgx_quotient_single_batch(self.h, _p(c) if n else None, n, stride, _p(z), batch,
+                                              _p(q) if n > 1 else None, _p(y)), "kzgx_quotient_single_batch")
+        return q, y
 
     def msm_batch_device(self, d_scalars: int, n: int, batch: int, stride: int, d_out: int, d_inf: int,
                          stream: int | None = None):
