@@ -60,8 +60,13 @@ def parse():
     ap.add_argument("--commit-first", action="store_true",
                     help="enqueue the commit batch before the proof batch (default: proofs first, so the "
                          "short quotient kernel is dispatched before the commit MSM fills the GPU)")
-    ap.add_argument("--cpu-sample", type=int, default=3, help="commits (+ as many proofs) timed on the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=12,
+                    help="commits (+ as many proofs) timed on the CPU oracle (~0.4 s each)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pippenger", action="store_true",
+                    help="skip the secondary Pippenger (table-less, create_commit's default) leg")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-call latency leg (benchmark/benchmark.cpp's timed regions)")
     return ap.parse_args()
 
 
@@ -128,6 +133,76 @@ def to_int(row):
     return sum(int(row[i]) << (64 * i) for i in range(len(row)))
 
 
+KERNELS = ("msm_count", "msm_scan", "msm_scatter", "msm_accum", "msm_reduce", "quotient_single")
+
+
+def timed_run(ctx, step, streams, steps, warmup, world, dist, torch, dev):
+    """W untimed warmup steps, then exactly K steps bracketed by a barrier +
+    synchronize on both sides; per-kernel HIP-event times (on each launch's
+    own stream) are collected inside the timed region.  Returns (elapsed s,
+    {kernel: (total ms, launches)}), elapsed = max over ranks."""
+    stream = streams[0]
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ctx.prof_clear()
+    ctx.prof_enable(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in streams[1:]:
+        if s is not stream:
+            s.wait_event(ev0)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ctx.prof_enable(False)
+    elapsed = t1 - t0
+    kern = {name: ctx.prof_read(name) for name in KERNELS}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kern
+
+
+def median_ms(f, reps):
+    f()  # warm (workspaces, first-use tables)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        f()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e3
+
+
+def latency_leg(ctx, coeffs_h, reps=7):
+    """The reference's own timed regions (benchmark/benchmark.cpp:46-52 and
+    :73-82), one call each through the C ABI entry points the C++ facade
+    calls (host buffers in, result on the host): create_commit of a
+    degree-4096 polynomial, create_proof(poly, 0, 1), and the multi-point
+    create_proof(poly, 0, N) on a 4096-coefficient polynomial."""
+    P = coeffs_h[0]
+    z0 = np.zeros((1, 4), dtype=np.uint64)
+    out = {"commit_ms": median_ms(lambda: ctx.msm(P), reps),
+           "proof_ms": median_ms(lambda: ctx.prove_single_batch(P, z0), reps)}
+    multi = {}
+    for N in (128, 256, 512, 1024, 2048, 4096):
+        xs = np.zeros((N, 4), dtype=np.uint64)
+        xs[:, 0] = np.arange(N, dtype=np.uint64)
+        multi[str(N)] = median_ms(lambda: ctx.prove_range(P[:4096], xs), 3)
+    out["multi_proof_ms"] = multi
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,15 +231,6 @@ def main():
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, 5000)
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
-    t_setup = time.perf_counter()
-    if fixed_bits:
-        # precompute the signed-digit multiples of the 4097-point SRS prefix
-        # (setup time, like the reference's trusted_setup ctor; not timed)
-        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, n)
-        ctx.set_fixed_points_per_thread(args.fixed_ppt)
-    t_setup = time.perf_counter() - t_setup
-    fb = ctx.fixed_base_info()
     w64 = ctx.w64
 
     rng = np.random.default_rng(0x4B5A47 + rank)
@@ -185,14 +251,14 @@ def main():
     d_pout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
     d_pinf = torch.zeros((B,), dtype=torch.int32, device=dev)
     d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
-    # the commits and proofs of a step are independent: each batch is cut into
-    # `split` sub-batches on their own streams so the latency-bound phases
-    # (bucket sums, tails) of one overlap the accumulation of another
+    # the commits and proofs of a step are independent batches: each runs on
+    # its own stream (optionally cut into `split` sub-batches) so the short
+    # latency-bound phases of one (reduction, affine conversion, quotient)
+    # overlap the accumulation of the other
     S = max(1, args.split)
     streams = [torch.cuda.Stream(device=dev) for _ in range(2 * S)]
     if args.serial:
         streams = [streams[0]] * (2 * S)
-    stream = streams[0]
     cstride = 0 if args.workload == "cfg3" else n
     cut = [B * s // S for s in range(S + 1)]
 
@@ -217,46 +283,35 @@ def main():
                 f()
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    ctx.prof_clear()
-    ctx.prof_enable(True)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for s in streams[1:]:
-        if s is not stream:
-            s.wait_event(ev0)
-    for _ in range(args.steps):
-        step()
-    for s in streams[1:]:
-        ev_b = torch.cuda.Event()
-        ev_b.record(s)
-        stream.wait_event(ev_b)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    ctx.prof_enable(False)
-    elapsed = t1 - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    kern = {}
-    for name in ("msm_count", "msm_scan", "msm_scatter", "msm_accum", "msm_reduce", "quotient_single"):
-        ms, cnt = ctx.prof_read(name)
-        kern[name] = (ms, cnt)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # ---- secondary legs on the default product path (no table): what
+    # kzg::trusted_setup::create_commit / create_proof do without precompute()
+    pip = None
+    if fixed_bits and not args.no_pippenger:
+        pe, pk = timed_run(ctx, step, streams, max(3, min(args.steps, 6)), 1, world, dist, torch, dev)
+        ps = max(3, min(args.steps, 6))
+        pip = {"value": units_per_step * ps * world / pe, "ms_per_step": pe / ps * 1e3,
+               "msm": "pippenger, c=%d, segment %d" % (args.window_bits, args.segment),
+               "kernel_ms_per_step": {k: v[0] / ps for k, v in pk.items()}}
+    lat = None
+    if not args.no_latency and args.workload != "cfg3":
+        lat = {"pippenger": latency_leg(ctx, coeffs_h)}
+
+    t_setup = time.perf_counter()
+    if fixed_bits:
+        # precompute the signed-digit multiples of the 4097-point SRS prefix
+        # (setup time, like the reference's trusted_setup ctor; not timed)
+        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, n)
+    t_setup = time.perf_counter() - t_setup
+    fb = ctx.fixed_base_info()
+    if fb[0] and lat is not None:
+        ctx.set_fixed_points_per_thread(0)  # single calls: spread the few MSMs over the GPU
+        lat["fixed_table"] = latency_leg(ctx, coeffs_h)
+    if fb[0]:
+        ctx.set_fixed_points_per_thread(args.fixed_ppt)
+
+    elapsed, kern = timed_run(ctx, step, streams, args.steps, args.warmup, world, dist, torch, dev)
 
     # ---- parity spot check (oracle identity, MSM-independent) ----
     checked = ok = 0
@@ -293,12 +348,12 @@ def main():
         tc0 = time.perf_counter()
         nunits = 0
         for i in range(s):
-            P = [to_int(row) for row in polys[i]]
             if args.workload != "cfg3":
                 corc.msm_naive(curve, srs, polys[i])  # create_commit
                 nunits += 1
-            q = K.proof_quotient(C, P, int(zs_h[i, 0]), 1)
-            corc.msm_naive(curve, srs[: max(len(q), 1)], corc.ints_to_limbs(q, 4))  # create_proof
+            # create_proof(poly, z, 1): evaluate + interpolate + (P - I) / Z in C, then the naive MSM
+            q = corc.quotient(curve, corc.limbs_to_ints(polys[i]), int(zs_h[i, 0]), 1)
+            corc.msm_naive(curve, srs[: max(len(q), 1)], corc.ints_to_limbs(q, 4))
             nunits += 1
         tcpu = time.perf_counter() - tc0
         cpu_model = platform.processor()
@@ -312,17 +367,20 @@ def main():
             pass
         cpu = {
             "value": nunits / tcpu,
-            "unit": "commits+proofs/s",
+            "unit": "commits+proofs/s" if args.workload != "cfg3" else "proofs/s",
             "cores": 1,
             "kind": "port",
-            "sample": "%d %s at degree %d on the C restatement of the reference's naive per-term polyeval_G1 "
-                      "(oracle/kzg_oracle.c), 1 thread, %s, %.1f s" % (
+            "sample": "%d %s at degree %d on the C restatement of the reference path (oracle/kzg_oracle.c: "
+                      "naive per-term polyeval_G1 with left-to-right double-and-add scalar multiplication in "
+                      "Jacobian coordinates, no GLV; quotient by evaluate + interpolate + long division), "
+                      "1 thread, %s, %.1f s" % (
                           nunits, "proofs" if args.workload == "cfg3" else "commits+proofs", degree, cpu_model,
                           tcpu),
         }
 
     if rank == 0:
         acc_ms, acc_cnt = kern["msm_accum"]
+        ms_per_step = elapsed / args.steps * 1e3
         # algorithmic bytes per MSM unit: n (affine point + 32 B scalar) + affine out
         P_b = 2 * w64 * 8
         unit_bytes_commit = n * (P_b + 32) + P_b
@@ -331,36 +389,23 @@ def main():
         launches_per_step = 1 if args.workload == "cfg3" else 2
         bytes_per_launch = per_step_bytes / launches_per_step
         avg_launch_ms = acc_ms / max(acc_cnt, 1)
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if acc_cnt else None
+        overlapped = not args.serial and launches_per_step > 1
+        if not overlapped and acc_cnt:
+            # one stream: the accumulation launches are disjoint in time
+            assert launches_per_step * avg_launch_ms <= ms_per_step * 1.02, (avg_launch_ms, ms_per_step)
+        # achieved: algorithmic bytes of the step / step time -- never a
+        # per-launch duration, which the second stream's launch inflates
+        achieved = per_step_bytes / (ms_per_step * 1e-3) / 1e9
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
         if os.path.exists(tpath):
             try:
                 with open(tpath) as f:
                     tj = json.load(f)
-                if tj.get("batch") == B:
+                if tj.get("batch") == B and tj.get("fixed_bits") == fb[0]:
                     traffic = tj.get("msm_accum_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        valu = None
-        vpath = os.path.join(ROOT, "profiles", "pmc_valu_cfg2.json")
-        if os.path.exists(vpath) and acc_cnt and curve == "BN254":
-            try:
-                with open(vpath) as f:
-                    vj = json.load(f)
-                # VALU issue roofline of the accumulation kernel: PMC instruction
-                # count per launch x launches per step / measured step time (the
-                # two streams' launches overlap, so per-launch event time would
-                # double-count), against 1024 SIMDs x 2.4 GHz / (measured mix
-                # cost per instruction)
-                ipl = vj["valu_insts_per_launch"] * B / vj["batch"]  # one launch = B MSMs of ~4097 points
-                rate = ipl * launches_per_step / (elapsed / args.steps)
-                peak = 256 * 4 * 2.4e9 / vj["mix_cost_cycles_per_inst"]
-                valu = {"wave_insts_per_s": rate, "peak_wave_insts_per_s": peak, "frac": rate / peak,
-                        "insts_per_wave_mixed_add": vj["valu_insts_per_wave_mixed_add"],
-                        "source": "profiles/pmc_valu_cfg2.json (PMC SQ_INSTS_VALU) x launches / live step time"}
-            except (OSError, ValueError, KeyError):
-                valu = None
         total_units = units_per_step * args.steps * world
         value = total_units / elapsed
         if fb[0]:
@@ -368,6 +413,12 @@ def main():
         else:
             wins = (257 + args.window_bits - 1) // args.window_bits
         madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * wins
+        madd_rate = madds / (ms_per_step * 1e-3)
+        peak = None
+        try:
+            peak = ctx.microbench_mixed_add()
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the headline
+            print("bench: mixed-add microbenchmark unavailable: %s" % e, file=sys.stderr)
         line = {
             "metric": "KZG commits/sec + proofs/sec, %s degree-4096" % curve,
             "value": value,
@@ -375,9 +426,10 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
+            # 0.905 commits/s + 0.925 proofs/s (README.md:132) -> 2 units per 2.185 s
             "vs_baseline": (value / (2.0 / (REF_COMMIT_S + REF_PROOF_S))) if args.workload == "cfg2" else None,
             "dtype": "u32 (radix-2^29 Montgomery limbs, %d-bit Fp)" % (254 if curve == "BN254" else 381),
             "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 from fixed tau",
@@ -401,24 +453,39 @@ def main():
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "algorithmic_bytes_per_step": per_step_bytes,
+                "launches_per_step": launches_per_step,
                 "avg_launch_ms": avg_launch_ms,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "note": "integer-VALU bound (no MFMA); see secondary",
+                "achieved_from": "algorithmic bytes per step / ms_per_step" + (
+                    " (the commit and proof launches overlap on two streams, so avg_launch_ms is not an isolated "
+                    "duration; profiles/*serial* hold the one-stream rocprof run)" if overlapped else ""),
+                "note": "integer-VALU bound (no MFMA); see secondary.valu_roofline",
             },
             "secondary": {
-                "msm_accum_mixed_adds_per_s": madds / (acc_ms * 1e-3 / max(acc_cnt, 1) * launches_per_step)
-                if acc_cnt else None,
+                "mixed_adds_per_s": madd_rate,
                 "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
-                "event_ms_total": ev_ms,
                 "fixed_table_setup_s": t_setup if fb[0] else None,
-                "valu_roofline": valu,
+                "fixed_table_bytes": fb[2] if fb[0] else None,
+                "valu_roofline": None if not peak else {
+                    "achieved_mixed_adds_per_s": madd_rate,
+                    "peak_mixed_adds_per_s": peak,
+                    "frac": madd_rate / peak,
+                    "peak_from": "kzgx_microbench_mixed_add: the accumulation loop's XYZZ mixed add on "
+                                 "register-resident operands at the kernel's occupancy, whole GPU, measured live",
+                },
+                "pippenger": pip,
+                "latency": lat,
             },
             "parity": {"checked": checked, "ok": int(ok), "method": "[P(tau)]G1 / [q(tau)]G1 identity"},
             "cpu_baseline": cpu,
-            "reference_published": {"commits_per_s": 1 / REF_COMMIT_S, "proofs_per_s": 1 / REF_PROOF_S,
-                                    "source": "README.md:132 (unstated CPU, 1 thread)"},
+            "reference_published": {"commit_ms": REF_COMMIT_S * 1e3, "proof_ms": REF_PROOF_S * 1e3,
+                                    "multi_proof_ms": {"128": 922.247, "256": 860.305, "512": 810.811,
+                                                       "1024": 800.158, "2048": 745.346},
+                                    "source": "README.md:127-139 (BN254, unstated CPU, 1 thread); "
+                                              "throughput equivalent %.3f commits+proofs/s" % (
+                                                  2.0 / (REF_COMMIT_S + REF_PROOF_S))},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -30,6 +30,10 @@
  *     names it.  The C++ facade (include/kzg.h) maps statuses onto the
  *     reference's exception types.
  *   - one context per thread (contexts are not internally locked).
+ *   - a context keeps MSM workspaces for up to 8 streams at once, so calls
+ *     on different streams run concurrently; a 9th distinct stream takes
+ *     over the least recently bound workspace after a device-wide
+ *     synchronisation (correct, but serialising: reuse streams).
  */
 #ifndef KZG_GPU_H
 #define KZG_GPU_H
@@ -97,6 +101,11 @@ int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* 
  * (0 = automatic, the default: 16 for batches of >= 64 MSMs, else enough
  * threads to fill the GPU, with a wavefront-level fold for single MSMs) */
 int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p);
+/* measurement: mixed additions per second of the MSM accumulation loop
+ * (the XYZZ mixed add k_fixed_accum inlines, same waves per SIMD) on
+ * L1-resident operands over the whole GPU -- the VALU ceiling the bench's
+ * valu_roofline divides by.  Needs an SRS (its first points are the operands). */
+int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s);
 
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */

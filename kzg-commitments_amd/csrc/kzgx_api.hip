@@ -243,6 +243,13 @@ int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* 
   return KZGX_OK;
 }
 
+int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s) {
+  KZGX_TRY(activate(ctx));
+  if (!adds_per_s) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return kzgx::microbench_mixed_add(&ctx->c, adds_per_s);
+}
+
 int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p) {
   KZGX_TRY(activate(ctx));
   if (p > 1024) return KZGX_ERR_ARG;  // 0 = automatic
@@ -554,39 +561,66 @@ int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx
   for (size_t k = 0; k < nctx; k++) {
     kzgx_ctx* c = ctxs[k];
     if (!c || c->c.curve != ctxs[0]->c.curve) return KZGX_ERR_ARG;
+    for (size_t j = 0; j < k; j++)
+      if (ctxs[j] == c) return KZGX_ERR_ARG;  // shards share per-context staging: one slice per context
     if (c->c.n_srs == 0) return KZGX_ERR_NO_SRS;
     if (starts[k] != (k == 0 ? 0 : starts[k - 1] + ctxs[k - 1]->c.n_srs)) return KZGX_ERR_ARG;  // contiguous
     cnt[k] = starts[k] >= n ? 0 : std::min(n - starts[k], c->c.n_srs);
   }
   if (starts[nctx - 1] + ctxs[nctx - 1]->c.n_srs < n) return KZGX_ERR_DEGREE;
   const size_t pb = point_words(ctxs[0]) * 4;
-  std::vector<void*> outs(nctx, nullptr);
-  // every shard's partial MSM, enqueued on its own context's stream
+  kzgx_ctx* c0 = ctxs[0];
+  // the fold's inputs live on ctxs[0]'s device: nctx partial points
+  // (all-zero = infinity: empty shards contribute nothing) + their flags
+  void *d_gather, *d_res;
+  KZGX_TRY(activate(c0));
+  KZGX_TRY(stage(c0, 2, nctx * (pb + 4) + 16, &d_gather));
+  KZGX_TRY(stage(c0, 3, pb + 16, &d_res));
+  uint32_t* d_flags = (uint32_t*)((char*)d_gather + nctx * pb);
+  KZGX_TRY_HIP(hipMemsetAsync(d_gather, 0, nctx * (pb + 4), c0->c.stream));
+  hipEvent_t zeroed;
+  KZGX_TRY_HIP(hipEventCreateWithFlags(&zeroed, hipEventDisableTiming));
+  std::vector<hipEvent_t> done;
+  struct EvGuard {
+    std::vector<hipEvent_t>* v;
+    hipEvent_t z;
+    ~EvGuard() {
+      for (auto e : *v) (void)hipEventDestroy(e);
+      (void)hipEventDestroy(z);
+    }
+  } evg{&done, zeroed};
+  KZGX_TRY_HIP(hipEventRecord(zeroed, c0->c.stream));
+  // every shard's partial MSM on its own context's stream, then a
+  // device-to-device (peer) copy of the partial point to ctxs[0]: no host
+  // round trip between the partial MSMs and the fold
   for (size_t k = 0; k < nctx; k++) {
     if (!cnt[k]) continue;
     kzgx_ctx* c = ctxs[k];
     KZGX_TRY(activate(c));
-    void* d_s;
+    void *d_s, *d_o;
     KZGX_TRY(stage(c, 0, cnt[k] * 32, &d_s));
-    KZGX_TRY(stage(c, 1, pb + 16, &outs[k]));
+    KZGX_TRY(stage(c, 1, pb + 16, &d_o));
     KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars + starts[k] * 4, cnt[k] * 32, hipMemcpyHostToDevice, c->c.stream));
-    KZGX_TRY(kzgx::msm_batch(&c->c, (const uint32_t*)d_s, cnt[k], 1, cnt[k] * 8, (uint32_t*)outs[k],
-                             (uint32_t*)((char*)outs[k] + pb), c->c.stream));
+    KZGX_TRY(kzgx::msm_batch(&c->c, (const uint32_t*)d_s, cnt[k], 1, cnt[k] * 8, (uint32_t*)d_o,
+                             (uint32_t*)((char*)d_o + pb), c->c.stream));
+    KZGX_TRY_HIP(hipStreamWaitEvent(c->c.stream, zeroed, 0));
+    KZGX_TRY_HIP(hipMemcpyPeerAsync((char*)d_gather + k * pb, c0->c.device, d_o, c->c.device, pb, c->c.stream));
+    KZGX_TRY_HIP(hipMemcpyPeerAsync(d_flags + k, c0->c.device, (char*)d_o + pb, c->c.device, 4, c->c.stream));
+    hipEvent_t e;
+    KZGX_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    done.push_back(e);
+    KZGX_TRY_HIP(hipEventRecord(e, c->c.stream));
   }
-  // gather the partial points, then one exact fold on ctxs[0]
-  std::vector<uint64_t> pts(nctx * pb / 8, 0);
-  std::vector<int> infs(nctx, 1);
-  for (size_t k = 0; k < nctx; k++) {
-    if (!cnt[k]) continue;
-    kzgx_ctx* c = ctxs[k];
-    KZGX_TRY(activate(c));
-    uint32_t oi = 1;
-    KZGX_TRY_HIP(hipMemcpyAsync(pts.data() + k * pb / 8, outs[k], pb, hipMemcpyDeviceToHost, c->c.stream));
-    KZGX_TRY_HIP(hipMemcpyAsync(&oi, (char*)outs[k] + pb, 4, hipMemcpyDeviceToHost, c->c.stream));
-    KZGX_TRY_HIP(hipStreamSynchronize(c->c.stream));
-    infs[k] = (int)oi;
-  }
-  return kzgx_g1_sum(ctxs[0], pts.data(), infs.data(), nctx, out_xy, out_is_inf);
+  KZGX_TRY(activate(c0));
+  for (auto e : done) KZGX_TRY_HIP(hipStreamWaitEvent(c0->c.stream, e, 0));
+  uint32_t* d_oi = (uint32_t*)((char*)d_res + pb);
+  KZGX_TRY(kzgx::g1_sum(&c0->c, (const uint32_t*)d_gather, d_flags, nctx, (uint32_t*)d_res, d_oi, c0->c.stream));
+  uint32_t oi = 0;
+  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_res, pb, hipMemcpyDeviceToHost, c0->c.stream));
+  KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, c0->c.stream));
+  KZGX_TRY_HIP(hipStreamSynchronize(c0->c.stream));
+  *out_is_inf = (int)oi;
+  return KZGX_OK;
 }
 
 /* ---- verify half: G2 SRS, polyeval_G2, pairing, verify_proof ---------------- */

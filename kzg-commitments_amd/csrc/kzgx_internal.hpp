@@ -44,6 +44,7 @@ struct MsmWs {
          rt_b = 0, q_b = 0, parts_b = 0, fpart_b = 0, fsum_b = 0;
   hipStream_t owner = nullptr;  // workspaces are per stream so calls on
   bool used = false;            // different streams may run concurrently
+  uint64_t bound_at = 0;        // Ctx::ws_clock when bound to owner
 };
 
 constexpr int KZGX_MAX_STREAMS = 8;
@@ -81,8 +82,12 @@ struct Ctx {
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];
   FixedTable fixed;
-  // the workspace bound to stream st (claimed on first use); nullptr when
-  // more than KZGX_MAX_STREAMS distinct streams are used
+  // the workspace bound to stream st (claimed on first use).  With more
+  // than KZGX_MAX_STREAMS distinct streams the least recently bound slot is
+  // rebound after a device synchronisation (its previous owner's work has
+  // then finished, so nothing still reads the buffers); nullptr only if that
+  // synchronisation fails.
+  uint64_t ws_clock = 0;
   MsmWs* ws_for(hipStream_t st) {
     for (auto& w : ws)
       if (w.used && w.owner == st) return &w;
@@ -90,9 +95,16 @@ struct Ctx {
       if (!w.used) {
         w.used = true;
         w.owner = st;
+        w.bound_at = ++ws_clock;
         return &w;
       }
-    return nullptr;
+    MsmWs* lru = &ws[0];
+    for (auto& w : ws)
+      if (w.bound_at < lru->bound_at) lru = &w;
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    lru->owner = st;
+    lru->bound_at = ++ws_clock;
+    return lru;
   }
   bool prof_on = false;
   std::vector<ProfRec> prof;
@@ -140,6 +152,8 @@ bool fixed_usable(const Ctx* ctx, size_t n);
 int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out);
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
+// mixed additions / s of the fixed-base accumulation loop on L1-resident operands (msm_fixed.hip)
+int microbench_mixed_add(Ctx* ctx, double* rate);
 // one workgroup sums count XYZZ points -> canonical affine (msm.hip)
 int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,

@@ -362,20 +362,32 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   const uint64_t H = 1ull << (c - 1);
   const size_t PB = packed_words<C>() * sizeof(uint32_t);
   const size_t bytes = (size_t)W * n * H * PB;
-  // drop the old table first: the new one may need most of the device
-  if (ft.d) {
+  // drop the old table (and its infinity flags) first: the new one may need
+  // most of the device
+  if (ft.d || ft.inf) {
     KZGX_TRY_HIP(hipDeviceSynchronize());
-    KZGX_TRY_HIP(hipFree(ft.d));
-    ft.d = nullptr;
-    ft.bytes = 0;
+    fixed_free(ctx);
   }
-  ft.n_t = 0;
+  // any failure below leaves no table (and no half-built allocation) behind
+  struct Guard {
+    Ctx* ctx;
+    uint32_t* bases = nullptr;
+    uint8_t* inf = nullptr;
+    bool ok = false;
+    ~Guard() {
+      if (bases) (void)hipFree(bases);
+      if (!ok) {
+        if (inf) (void)hipFree(inf);
+        fixed_free(ctx);
+      }
+    }
+  } g{ctx};
   KZGX_TRY_HIP(hipMalloc((void**)&ft.d, bytes));
   ft.bytes = bytes;
-  uint32_t* d_bases = nullptr;
-  uint8_t* d_inf = nullptr;
-  KZGX_TRY_HIP(hipMalloc((void**)&d_bases, (size_t)W * n * PB));
-  KZGX_TRY_HIP(hipMalloc((void**)&d_inf, n));
+  KZGX_TRY_HIP(hipMalloc((void**)&g.bases, (size_t)W * n * PB));
+  KZGX_TRY_HIP(hipMalloc((void**)&g.inf, n));
+  uint32_t* d_bases = g.bases;
+  uint8_t* d_inf = g.inf;
   hipStream_t st = ctx->stream;
   hipLaunchKernelGGL(k_fixed_bases<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_canon, (uint32_t)n, W, c,
                      d_bases, d_inf);
@@ -394,7 +406,7 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
     KZGX_TRY_HIP(hipGetLastError());
     KZGX_TRY_HIP(hipStreamSynchronize(st));
   }
-  (void)hipFree(d_bases);
+  g.ok = true;
   ft.inf = d_inf;
   ft.c = c;
   ft.W = W;
@@ -505,6 +517,78 @@ int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
   return ctx->curve == KZGX_CURVE_BN254
              ? fixed_msm_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out)
              : fixed_msm_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
+}
+
+// --------------------------------------------------------------------------
+// measured VALU peak of the accumulation loop (the denominator of the bench's
+// valu_roofline): k_fixed_accum's inlined XYZZ mixed addition, with the same
+// launch bounds (waves per SIMD), over operands that stay in L1 (a 64-point
+// table: no HBM stream, no digit logic), whole GPU, ITER additions per thread
+// --------------------------------------------------------------------------
+template <class C>
+__global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_microbench_madd(const uint32_t* __restrict__ pts,
+                                                                                uint32_t iters,
+                                                                                uint32_t* __restrict__ sink) {
+  constexpr int PW = affine_words<C>();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  Xyzz<C> acc = xyzz_from_affine<C>(affine_load<C>(pts + (size_t)(t & 63) * PW));
+#pragma unroll 1
+  for (uint32_t k = 0; k < iters; k++) {
+    Affine<C> a = affine_load<C>(pts + (size_t)((t + 1 + k) & 63) * PW);
+    acc = xyzz_add_affine_impl<C>(acc, a);
+  }
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < C::Fp29::L; i++) o ^= acc.X.v[i] ^ acc.ZZ.v[i];
+  if (o == 0x9e3779b9u) sink[t] = o;  // keeps the chain live; practically never stores
+}
+
+// mixed additions per second: 64 distinct multiples of the SRS's first point
+// (built with the table kernels' own arithmetic), then a timed launch
+template <class C>
+static int microbench_madd_impl(Ctx* ctx, double* rate) {
+  if (ctx->n_srs == 0) return KZGX_ERR_NO_SRS;
+  constexpr int PW = affine_words<C>();
+  hipStream_t st = ctx->stream;
+  uint32_t *d_pts = nullptr, *d_sink = nullptr;
+  const uint32_t waves = 256 * 4 * fixed_accum_waves<C>() * 4;  // four full residencies
+  const uint32_t iters = 192;
+  KZGX_TRY_HIP(hipMalloc((void**)&d_pts, 64 * PW * 4));
+  struct Free {
+    uint32_t** a;
+    uint32_t** b;
+    ~Free() {
+      if (*a) (void)hipFree(*a);
+      if (*b) (void)hipFree(*b);
+    }
+  } fr{&d_pts, &d_sink};
+  KZGX_TRY_HIP(hipMalloc((void**)&d_sink, (size_t)waves * 64 * 4));
+  // T[0][i] holds the SRS points in the 80 / 112 B radix-2^29 layout; the
+  // first 64 points (or repeats of them) are distinct curve points
+  for (uint32_t i = 0; i < 64; i++)
+    KZGX_TRY_HIP(hipMemcpyAsync(d_pts + (size_t)i * PW, ctx->d_table + (size_t)(i % ctx->n_srs) * PW, PW * 4,
+                                hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(k_microbench_madd<C>, dim3(waves), dim3(64), 0, st, d_pts, 8u, d_sink);  // warm
+  hipEvent_t a, b;
+  KZGX_TRY_HIP(hipEventCreate(&a));
+  KZGX_TRY_HIP(hipEventCreate(&b));
+  KZGX_TRY_HIP(hipEventRecord(a, st));
+  hipLaunchKernelGGL(k_microbench_madd<C>, dim3(waves), dim3(64), 0, st, d_pts, iters, d_sink);
+  KZGX_TRY_HIP(hipEventRecord(b, st));
+  KZGX_TRY_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  hipError_t e = hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  KZGX_TRY_HIP(e);
+  KZGX_TRY_HIP(hipGetLastError());
+  *rate = (double)waves * 64 * iters / (ms * 1e-3);
+  return KZGX_OK;
+}
+
+int microbench_mixed_add(Ctx* ctx, double* rate) {
+  return ctx->curve == KZGX_CURVE_BN254 ? microbench_madd_impl<BN254G1>(ctx, rate)
+                                        : microbench_madd_impl<BLS12381G1>(ctx, rate);
 }
 
 }  // namespace kzgx

@@ -356,29 +356,15 @@ static int interpolate_impl(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, 
 }
 
 template <class FR>
+static uint32_t* vanishing_mont(const uint32_t* d_x, size_t n, uint32_t* ws, hipStream_t st);
+
+template <class FR>
 static int vanishing_impl(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipStream_t st) {
   constexpr int N = FR::N;
   const size_t eb = N * sizeof(uint32_t);
-  const size_t lvl_elems = 2 * n + 2;
-  char* base;
-  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws, (n + 2 * lvl_elems) * eb, &ctx->poly_ws_b));
-  base = (char*)ctx->d_poly_ws;
-  uint32_t* xm = (uint32_t*)base;
-  uint32_t* L0 = xm + n * N;
-  uint32_t* L1 = L0 + lvl_elems * N;
-  const unsigned g1 = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(k_to_mont<FR>, dim3(g1), dim3(256), 0, st, d_x, xm, (uint32_t)n);
-  hipLaunchKernelGGL(k_tree_leaves<FR>, dim3(g1), dim3(256), 0, st, xm, (uint32_t)n, L0);
-  uint32_t* cur = L0;
-  uint32_t* nxt = L1;
-  for (size_t s = 1; s < n; s *= 2) {
-    size_t nslots_out = (n + 2 * s - 1) / (2 * s);
-    size_t waves = nslots_out * (2 * s + 1);
-    hipLaunchKernelGGL(k_tree_mul<FR>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, cur, (uint32_t)s,
-                       (uint32_t)n, nxt, (uint32_t)nslots_out);
-    std::swap(cur, nxt);
-  }
-  hipLaunchKernelGGL(k_from_mont<FR>, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, cur, d_Z,
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws, (n + 2 * (2 * n + 2)) * eb, &ctx->poly_ws_b));
+  uint32_t* Z = vanishing_mont<FR>(d_x, n, (uint32_t*)ctx->d_poly_ws, st);
+  hipLaunchKernelGGL(k_from_mont<FR>, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st, Z, d_Z,
                      (uint32_t)(n + 1));
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
@@ -398,38 +384,81 @@ int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t 
 // --------------------------------------------------------------------------
 // multi-point opening: q = (P - I) / Z  (trusted_setup.cpp:225, NTL sub + div)
 // --------------------------------------------------------------------------
-// out[i] = A[i] - B[i] for i < nout (missing coefficients are zero)
+// out[j] = in[n_in - 1 - j] for j < cnt (zero where the source index is
+// negative): the reversal X^(n_in - 1) A(1 / X), truncated to cnt terms
 template <class FR>
-__global__ void k_fr_sub(const uint32_t* __restrict__ A, uint32_t na, const uint32_t* __restrict__ B, uint32_t nb,
-                         uint32_t* __restrict__ out, uint32_t nout) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nout) return;
-  Fe<FR> a = i < na ? fe_load<FR>(A + (size_t)i * FR::N) : fe_zero<FR>();
-  Fe<FR> b = i < nb ? fe_load<FR>(B + (size_t)i * FR::N) : fe_zero<FR>();
-  fe_store<FR>(out + (size_t)i * FR::N, fe_sub<FR>(a, b));
+__global__ void k_fr_rev(const uint32_t* __restrict__ in, uint32_t n_in, uint32_t* __restrict__ out, uint32_t cnt) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cnt) return;
+  fe_store<FR>(out + (size_t)j * FR::N, j < n_in ? fe_load<FR>(in + (size_t)(n_in - 1 - j) * FR::N) : fe_zero<FR>());
 }
 
-// Quotient of A (na coefficients, overwritten as the remainder) by the monic
-// Z (nz + 1 coefficients): schoolbook long division from the top, one
-// workgroup, the nz coefficient updates of each step spread over its threads.
+// truncated product, one wavefront per output coefficient:
+//   out[k] = (neg ? -1 : 1) sum_{i + j = k - shift} A_i B_j,   k in [k0, k1)
+// A_i (i < na) and B_j (j < nb); one operand canonical and the other in
+// Montgomery form gives a canonical result (both Montgomery: Montgomery).
 template <class FR>
-__global__ __launch_bounds__(1024) void k_div_monic(uint32_t* __restrict__ rem, uint32_t na,
-                                                    const uint32_t* __restrict__ Z, uint32_t nz,
-                                                    uint32_t* __restrict__ q) {
+__global__ __launch_bounds__(256) void k_conv(const uint32_t* __restrict__ A, uint32_t na,
+                                              const uint32_t* __restrict__ B, uint32_t nb, uint32_t* __restrict__ out,
+                                              uint32_t k0, uint32_t k1, uint32_t shift, int neg) {
   constexpr int N = FR::N;
-  const uint32_t nq = na - nz;
-  for (uint32_t k = nq; k-- > 0;) {
-    const Fe<FR> qk = fe_load<FR>(rem + (size_t)(k + nz) * N);
-    if (threadIdx.x == 0) fe_store<FR>(q + (size_t)k * N, qk);
-    const Fe<FR> qm = fe_to_mont<FR>(qk);
-    for (uint32_t j = threadIdx.x; j < nz; j += blockDim.x) {
-      uint32_t* r = rem + (size_t)(k + j) * N;
-      fe_store<FR>(r, fe_sub<FR>(fe_load<FR>(r), fe_mul<FR>(fe_load<FR>(Z + (size_t)j * N), qm)));
-    }
-    __syncthreads();
-  }
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t k = k0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= k1) return;  // whole wavefront
+  const uint32_t t = k - shift;
+  const uint32_t i0 = t + 1 > nb ? t + 1 - nb : 0, i1 = min(t, na - 1);
+  Fe<FR> acc = fe_zero<FR>();
+  for (uint32_t i = i0 + lane; i <= i1; i += 64)
+    acc = fe_add<FR>(acc, fe_mul<FR>(fe_load<FR>(A + (size_t)i * N), fe_load<FR>(B + (size_t)(t - i) * N)));
+  acc = wave_sum<FR>(acc);
+  if (lane == 0) fe_store<FR>(out + (size_t)k * N, neg ? fe_neg<FR>(acc) : acc);
 }
 
+template <class FR>
+static void launch_conv(const uint32_t* A, size_t na, const uint32_t* B, size_t nb, uint32_t* out, size_t k0, size_t k1,
+                        size_t shift, bool neg, hipStream_t st) {
+  if (k1 <= k0) return;
+  hipLaunchKernelGGL(k_conv<FR>, dim3((unsigned)((k1 - k0 + 3) / 4)), dim3(256), 0, st, A, (uint32_t)na, B,
+                     (uint32_t)nb, out, (uint32_t)k0, (uint32_t)k1, (uint32_t)shift, neg ? 1 : 0);
+}
+
+// vanishing polynomial Z = prod (X - x_i) in Montgomery form (product tree
+// over the context's scratch); returns the slot holding Z's n + 1
+// coefficients.  ws must hold n + 2 (2 n + 2) elements.
+template <class FR>
+static uint32_t* vanishing_mont(const uint32_t* d_x, size_t n, uint32_t* ws, hipStream_t st) {
+  constexpr int N = FR::N;
+  const size_t lvl_elems = 2 * n + 2;
+  uint32_t* xm = ws;
+  uint32_t* L0 = xm + n * N;
+  uint32_t* L1 = L0 + lvl_elems * N;
+  const unsigned g1 = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_to_mont<FR>, dim3(g1), dim3(256), 0, st, d_x, xm, (uint32_t)n);
+  hipLaunchKernelGGL(k_tree_leaves<FR>, dim3(g1), dim3(256), 0, st, xm, (uint32_t)n, L0);
+  uint32_t* cur = L0;
+  uint32_t* nxt = L1;
+  for (size_t s = 1; s < n; s *= 2) {
+    size_t nslots_out = (n + 2 * s - 1) / (2 * s);
+    size_t waves = nslots_out * (2 * s + 1);
+    hipLaunchKernelGGL(k_tree_mul<FR>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, cur, (uint32_t)s,
+                       (uint32_t)n, nxt, (uint32_t)nslots_out);
+    std::swap(cur, nxt);
+  }
+  return cur;
+}
+
+// Multi-point quotient without interpolation.  For the points x_0..x_{N-1},
+// I = P mod Z (I agrees with P on every x_i and deg I < N), so the
+// reference's (P - I) / Z (trusted_setup.cpp:225, NTL sub + div) is exactly
+// the polynomial quotient P div Z.  With m = n - N quotient coefficients and
+// rev_k(A) = X^k A(1/X):
+//   rev_{m-1}(q) = rev_{n-1}(P) * rev_N(Z)^-1  mod X^m
+// (the remainder term carries a factor X^m).  rev_N(Z) has constant term 1
+// (Z is monic), so its inverse mod X^m comes from Newton's iteration
+//   S_{2l} = S_l - S_l ((rev Z) S_l - 1)   mod X^{2l},
+// every step two truncated products of one wavefront per output coefficient
+// (BN254's r - 1 has 2-adicity 2: no NTT domain, and at these sizes the
+// parallel schoolbook products are a fraction of the MSM anyway).
 template <class FR>
 static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_x, size_t len,
                                  uint32_t* d_q, size_t* nq_out, hipStream_t st) {
@@ -437,22 +466,37 @@ static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const 
   const size_t eb = N * 4;
   *nq_out = 0;
   if (n <= len) return KZGX_OK;  // deg P < len: I = P, q = 0 (NTL normalizes to the zero polynomial)
-  // workspace: ys (len), I (len), Z (len + 1), A (n)  -- separate from the interpolation scratch
-  void* base;
-  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (3 * len + 1 + n) * eb, &ctx->poly_ws2_b));
-  base = ctx->d_poly_ws2;
-  uint32_t* ys = (uint32_t*)base;
-  uint32_t* I = ys + len * N;
-  uint32_t* Z = I + len * N;
-  uint32_t* A = Z + (len + 1) * N;
-  KZGX_TRY(poly_eval(ctx, d_P, n, d_x, len, ys, st));
-  KZGX_TRY(poly_interpolate(ctx, d_x, ys, len, I, st));
-  KZGX_TRY(poly_vanishing(ctx, d_x, len, Z, st));
-  hipLaunchKernelGGL(k_fr_sub<FR>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_P, (uint32_t)n, I,
-                     (uint32_t)len, A, (uint32_t)n);
-  hipLaunchKernelGGL(k_div_monic<FR>, dim3(1), dim3(1024), 0, st, A, (uint32_t)n, Z, (uint32_t)len, d_q);
+  const size_t m = n - len;
+  // workspace: tree (len + 2 (2 len + 2)), Rz, S, E, Prev, Qrev (m each)
+  const size_t tree = len + 2 * (2 * len + 2);
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (tree + 5 * m) * eb, &ctx->poly_ws2_b));
+  uint32_t* base = (uint32_t*)ctx->d_poly_ws2;
+  uint32_t* Zm = vanishing_mont<FR>(d_x, len, base, st);
+  uint32_t* Rz = base + tree * N;
+  uint32_t* S = Rz + m * N;
+  uint32_t* E = S + m * N;
+  uint32_t* Prev = E + m * N;
+  uint32_t* Qrev = Prev + m * N;
+  const size_t nrz = std::min(len + 1, m);
+  const unsigned gm = (unsigned)((m + 255) / 256);
+  hipLaunchKernelGGL(k_fr_rev<FR>, dim3((unsigned)((nrz + 255) / 256)), dim3(256), 0, st, Zm, (uint32_t)(len + 1), Rz,
+                     (uint32_t)nrz);
+  hipLaunchKernelGGL(k_fr_rev<FR>, dim3(gm), dim3(256), 0, st, d_P, (uint32_t)n, Prev, (uint32_t)m);
+  // S = 1 (Montgomery) mod X^1, then Newton to m terms
+  hipLaunchKernelGGL(k_fr_rev<FR>, dim3(1), dim3(64), 0, st, Zm + len * N, 1u, S, 1u);  // Z_len = 1 (monic)
+  for (size_t l = 1; l < m;) {
+    const size_t l2 = std::min(2 * l, m);
+    // E_k = ((rev Z) S)_k for k in [l, l2): the coefficients of (rev Z) S - 1 that are not yet zero
+    launch_conv<FR>(S, l, Rz, nrz, E, l, l2, 0, false, st);
+    // S_k = -(S (E X^l))_k = -sum_i S_i E_{k-i} for k in [l, l2)
+    launch_conv<FR>(S, l, E + l * N, l2 - l, S, l, l2, l, true, st);
+    l = l2;
+  }
+  // rev(q) = rev(P) S mod X^m (canonical * Montgomery = canonical), then q
+  launch_conv<FR>(Prev, m, S, m, Qrev, 0, m, 0, false, st);
+  hipLaunchKernelGGL(k_fr_rev<FR>, dim3(gm), dim3(256), 0, st, Qrev, (uint32_t)m, d_q, (uint32_t)m);
   KZGX_TRY_HIP(hipGetLastError());
-  *nq_out = n - len;
+  *nq_out = m;
   return KZGX_OK;
 }
 

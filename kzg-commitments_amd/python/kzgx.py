@@ -22,7 +22,7 @@ BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
-    "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_set_fixed_points_per_thread", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
@@ -50,6 +50,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libkzgx.so not built (run __graft_entry__.build())")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 with
+        # the same soname as /opt/rocm's.  Loaded first, torch's copy is the
+        # one libkzgx.so binds to; loaded second (after libkzgx pulled in
+        # /opt/rocm's), torch finds no devices.  Device pointers from torch
+        # tensors are then valid in both.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         sig = {
             "kzgx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -68,6 +77,7 @@ def lib():
             "kzgx_set_fixed_base": (ctypes.c_int, [vp, ctypes.c_int, sz]),
             "kzgx_fixed_base_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
             "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
+            "kzgx_microbench_mixed_add": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_gen_srs_g1": (ctypes.c_int, [vp, u64p, sz, sz]),
             "kzgx_get_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
@@ -190,6 +200,12 @@ class Context:
 
     def set_fixed_points_per_thread(self, p: int):
         _chk(lib().kzgx_set_fixed_points_per_thread(self.h, p), "kzgx_set_fixed_points_per_thread")
+
+    def microbench_mixed_add(self) -> float:
+        """mixed additions / s of the accumulation loop at full occupancy"""
+        r = ctypes.c_double(0)
+        _chk(lib().kzgx_microbench_mixed_add(self.h, ctypes.byref(r)), "kzgx_microbench_mixed_add")
+        return r.value
 
     def prof_clear(self):
         _chk(lib().kzgx_prof_clear(self.h), "kzgx_prof_clear")

@@ -138,3 +138,27 @@ def quotient(curve: str, coeffs, off: int, length: int) -> list:
     if rc != 0:
         raise ZeroDivisionError("quotient failed %d" % rc)
     return limbs_to_ints(out[:nq.value])
+
+
+def scalar_mul(curve: str, P, k: int):
+    """k P for an affine P = (x, y) (None = infinity); the C oracle's
+    double-and-add (orc_scalar_mul)."""
+    if P is None:
+        return None
+    nl = BASE_LIMBS[curve]
+    xy = points_to_array(curve, [P])[0].copy()
+    kk = ints_to_limbs([k], 4)[0].copy()
+    out = np.zeros(2 * nl, dtype=np.uint64)
+    inf = lib().orc_scalar_mul(CURVE_ID[curve], _p(xy), _p(kk), _p(out))
+    if inf < 0:
+        raise ValueError("bad curve")
+    return None if inf else array_to_points(curve, out[None, :])[0]
+
+
+def poly_eval(curve: str, coeff_limbs: np.ndarray, x: int) -> int:
+    """P(x) mod r by Horner in C; coeff_limbs: n x 4 canonical limbs"""
+    P = np.ascontiguousarray(coeff_limbs, dtype=np.uint64).reshape(-1, 4)
+    xx = ints_to_limbs([x], 4)[0].copy()
+    y = np.zeros(4, dtype=np.uint64)
+    lib().orc_poly_eval(CURVE_ID[curve], _p(P), P.shape[0], _p(xx), _p(y))
+    return limbs_to_ints(y[None, :])[0]
