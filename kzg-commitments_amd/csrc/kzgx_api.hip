@@ -149,7 +149,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   kzgx::fixed_free(&c);
   for (auto& w : c.ws) {
     void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
-                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum};
+                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate};
     for (void* p : wb)
       if (p) (void)hipFree(p);
   }
@@ -868,3 +868,29 @@ int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const in
 }
 
 }  // extern "C"
+
+// Debug only (not part of include/kzg_gpu.h): copy a Pippenger workspace
+// buffer of the context's default stream to the host, after a device sync.
+extern "C" int kzgx_debug_ws_read(kzgx_ctx* ctx, const char* name, void* host, size_t bytes) {
+  KZGX_TRY(activate(ctx));
+  kzgx::MsmWs* w = ctx->c.ws_for(ctx->c.stream);
+  if (!w || !name || !host) return KZGX_ERR_ARG;
+  const void* src = nullptr;
+  size_t cap = 0;
+  const std::string s(name);
+  if (s == "offsets") src = w->offsets, cap = w->offsets_b;
+  else if (s == "entries") src = w->entries, cap = w->entries_b;
+  else if (s == "bsum") src = w->bsum, cap = w->bsum_b;
+  else if (s == "sstate") src = w->sstate, cap = w->sstate_b;
+  else if (s == "tailk") src = w->tailk, cap = w->tailk_b;
+  else if (s == "heads") src = w->heads, cap = w->heads_b;
+  else if (s == "tails") src = w->tails, cap = w->tails_b;
+  else if (s == "counts") src = w->counts, cap = w->counts_b;
+  else if (s == "cursors") src = w->cursors, cap = w->cursors_b;
+  else if (s == "gmeta") src = w->gmeta, cap = w->gmeta_b;
+  else if (s == "gpart") src = w->gpart, cap = w->gpart_b;
+  if (!src || bytes > cap) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipDeviceSynchronize());
+  KZGX_TRY_HIP(hipMemcpy(host, src, bytes, hipMemcpyDeviceToHost));
+  return KZGX_OK;
+}

@@ -9,13 +9,17 @@
 //    so all windows of an MSM share ONE set of 2^(c-1) signed-digit buckets and
 //    there is no per-window doubling chain;
 //  * per MSM b: signed c-bit digits -> (point, sign) entries counting-sorted by
-//    bucket (LDS histograms + one global atomic per (workgroup, bucket));
+//    bucket: per-block LDS histograms, a 2-D scan into bucket offsets and
+//    per-block write bases, and a scatter ranked by LDS atomics alone (no
+//    global atomics anywhere in the sort);
 //  * bucket accumulation is load balanced: every thread owns exactly K
-//    consecutive sorted entries and does K mixed XYZZ additions; runs that
-//    cross a segment boundary leave head/tail partials that the reduction
-//    kernel merges;
-//  * the reduction (one workgroup per MSM) finishes the buckets, forms
-//    sum (k+1) B_k with an LDS suffix scan + tree, and converts to affine.
+//    consecutive sorted entries and does K mixed XYZZ additions; partials of
+//    buckets that cross segment boundaries are staged in LDS and merged
+//    inside the workgroup, only workgroup-crossing buckets go through HBM;
+//  * the bucket running sum sum_k (k+1) B_k: per-thread running sums over
+//    J = 8 buckets, then one wavefront per MSM folds the (R, T) pairs with a
+//    __shfl_down suffix scan and a shuffle-tree reduction, then converts to
+//    affine.
 // Every step is an exact group operation, so the affine output is bit-exact
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
@@ -101,45 +105,68 @@ KZGX_DEV void load_scalar(const uint32_t* p, uint32_t (&s)[8]) {
   s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
 }
 
-// pass 1: per-MSM bucket histogram
+// Scalars are recoded per (MSM, count block) of SORT_BLK consecutive points.
+// Each count block keeps its own bucket histogram, so the sort needs no
+// global atomics: the scan turns the histograms into bucket offsets and
+// per-block write bases, and the scatter ranks entries with LDS atomics only.
+#ifndef KZGX_SORT_SPT
+#define KZGX_SORT_SPT 2
+#endif
+constexpr uint32_t SORT_SPT = KZGX_SORT_SPT;  // scalars per thread in count / scatter
+constexpr uint32_t SORT_BLK = 256 * SORT_SPT;  // scalars per count block
+
+// pass 1: bucket histogram of every (MSM, count block), written in full
 template <int CB>
 __global__ __launch_bounds__(256) void k_msm_count(const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words,
-                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ counts,
-                                                   uint32_t point_base, uint32_t point_stride) {
+                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ bcount,
+                                                   uint32_t nblk, uint32_t point_base, uint32_t point_stride) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   __shared__ uint32_t hist[NB];
   const uint32_t b = blockIdx.y;
   for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && !inf[point_base + b * point_stride + i]) {
-    uint32_t s[8];
-    load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
-    uint32_t carry = 0;
+#pragma unroll 1
+  for (uint32_t j = 0; j < SORT_SPT; j++) {
+    const uint32_t i = blockIdx.x * SORT_BLK + j * 256 + threadIdx.x;
+    if (i < n && !inf[point_base + b * point_stride + i]) {
+      uint32_t s[8];
+      load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
+      uint32_t carry = 0;
 #pragma unroll
-    for (int w = 0; w < W; w++) {
-      int d = digit_at<CB>(s, w, carry);
-      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+      for (int w = 0; w < W; w++) {
+        int d = digit_at<CB>(s, w, carry);
+        if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+      }
     }
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) {
-    uint32_t h = hist[k];
-    if (h) atomicAdd(&counts[(size_t)b * NB + k], h);
-  }
+  uint32_t* out = bcount + ((size_t)b * nblk + blockIdx.x) * NB;
+  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) out[k] = hist[k];
 }
 
-// pass 2: exclusive scan of the histogram -> offsets[b][0..NB], cursors
-__global__ __launch_bounds__(256) void k_msm_scan(const uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
-                                                  uint32_t* __restrict__ cursors, uint32_t nb) {
+// pass 2, one workgroup per MSM: bucket totals over the count blocks, an
+// exclusive scan -> offsets[b][0..NB], and the write base of every
+// (count block, bucket): bbase[b][blk][k] = offsets[k] + sum_{blk' < blk} count
+template <int CB>
+__global__ __launch_bounds__(256) void k_msm_scan(const uint32_t* __restrict__ bcount, uint32_t nblk,
+                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ bbase) {
+  constexpr uint32_t NB = Win<CB>::NB;
+  constexpr uint32_t PER = NB / 256;  // NB is a multiple of 256 (c >= 9)
+  __shared__ uint32_t tot[NB];
   __shared__ uint32_t part[256];
   const uint32_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
-  const uint32_t per = nb / 256;  // nb is a multiple of 256
-  const uint32_t* cnt = counts + (size_t)b * nb;
+  const uint32_t* bc = bcount + (size_t)b * nblk * NB;
+  for (uint32_t k = t; k < NB; k += 256) {  // coalesced over k
+    uint32_t s = 0;
+    for (uint32_t blk = 0; blk < nblk; blk++) s += bc[(size_t)blk * NB + k];
+    tot[k] = s;
+  }
+  __syncthreads();
   uint32_t local = 0;
-  for (uint32_t j = 0; j < per; j++) local += cnt[t * per + j];
+#pragma unroll
+  for (uint32_t j = 0; j < PER; j++) local += tot[t * PER + j];
   part[t] = local;
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {
@@ -148,155 +175,406 @@ __global__ __launch_bounds__(256) void k_msm_scan(const uint32_t* __restrict__ c
     part[t] += v;
     __syncthreads();
   }
-  uint32_t run = part[t] - local;  // exclusive prefix
-  uint32_t* off = offsets + (size_t)b * (nb + 1);
-  uint32_t* cur = cursors + (size_t)b * nb;
-  for (uint32_t j = 0; j < per; j++) {
-    off[t * per + j] = run;
-    cur[t * per + j] = run;
-    run += cnt[t * per + j];
+  uint32_t run = part[t] - local;  // exclusive prefix of this thread's buckets
+#pragma unroll
+  for (uint32_t j = 0; j < PER; j++) {
+    const uint32_t c = tot[t * PER + j];
+    tot[t * PER + j] = run;
+    run += c;
   }
-  if (t == 255) off[nb] = run;
+  uint32_t* off = offsets + (size_t)b * (NB + 1);
+  if (t == 255) off[NB] = run;
+  __syncthreads();
+  uint32_t* bb = bbase + (size_t)b * nblk * NB;
+  for (uint32_t k = t; k < NB; k += 256) {
+    uint32_t base = tot[k];
+    off[k] = base;
+    for (uint32_t blk = 0; blk < nblk; blk++) {
+      bb[(size_t)blk * NB + k] = base;
+      base += bc[(size_t)blk * NB + k];
+    }
+  }
 }
 
-// pass 3: scatter (table index | sign) entries into bucket order
+// pass 3: scatter (table index | sign) entries into bucket order.  The block
+// first sorts its own entries in LDS (local offsets from its histogram,
+// ranks from LDS atomics), then writes them out in that order: lanes of a
+// wavefront write consecutive positions of one bucket's run, so the stores
+// coalesce instead of landing as scattered 4-byte writes.  No global atomics.
 template <int CB>
 __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
                                                      size_t stride_words, const uint8_t* __restrict__ inf,
-                                                     uint32_t* __restrict__ cursors, uint32_t* __restrict__ entries,
-                                                     size_t emax, uint32_t n_srs, uint32_t point_base,
-                                                     uint32_t point_stride) {
+                                                     const uint32_t* __restrict__ bcount,
+                                                     const uint32_t* __restrict__ bbase, uint32_t nblk,
+                                                     uint32_t* __restrict__ entries, size_t emax, uint32_t n_srs,
+                                                     uint32_t point_base, uint32_t point_stride) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
-  __shared__ uint32_t lcount[NB];
-  __shared__ uint32_t lbase[NB];
+  constexpr uint32_t PER = NB / 256;
+  __shared__ uint32_t stage[SORT_BLK * W];
+  __shared__ uint32_t lstart[NB + 1];
+  __shared__ uint32_t cur[NB];
+  __shared__ uint32_t part[256];
   const uint32_t b = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) lcount[k] = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  int dig[W];
-  uint32_t rank[W];
-  const uint32_t ig = point_base + b * point_stride + i;  // SRS index of this scalar
-  const bool live = i < n && !inf[ig];
-  if (live) {
-    uint32_t s[8];
-    load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
-    uint32_t carry = 0;
+  const uint32_t t = threadIdx.x;
+  const size_t hb = ((size_t)b * nblk + blockIdx.x) * NB;
+  // local exclusive scan of this block's histogram
+  uint32_t local = 0;
 #pragma unroll
-    for (int w = 0; w < W; w++) {
-      int d = digit_at<CB>(s, w, carry);
-      dig[w] = d;
-      rank[w] = d != 0 ? atomicAdd(&lcount[(d < 0 ? -d : d) - 1], 1u) : 0u;
-    }
+  for (uint32_t j = 0; j < PER; j++) {
+    const uint32_t c = bcount[hb + t * PER + j];
+    cur[t * PER + j] = c;
+    local += c;
   }
+  part[t] = local;
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < NB; k += blockDim.x) {
-    uint32_t h = lcount[k];
-    lbase[k] = h ? atomicAdd(&cursors[(size_t)b * NB + k], h) : 0u;
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    uint32_t v = (t >= d) ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
   }
-  __syncthreads();
-  if (live) {
-    uint32_t* out = entries + b * emax;
+  uint32_t run = part[t] - local;
 #pragma unroll
-    for (int w = 0; w < W; w++) {
-      int d = dig[w];
-      if (d != 0) {
-        uint32_t k = (uint32_t)((d < 0 ? -d : d) - 1);
-        out[lbase[k] + rank[w]] = ((uint32_t)w * n_srs + ig) | (d < 0 ? 0x80000000u : 0u);
+  for (uint32_t j = 0; j < PER; j++) {
+    const uint32_t c = cur[t * PER + j];
+    lstart[t * PER + j] = run;
+    cur[t * PER + j] = run;
+    run += c;
+  }
+  if (t == 255) lstart[NB] = run;
+  __syncthreads();
+  // rank every digit into the block's LDS stage
+#pragma unroll 1
+  for (uint32_t j = 0; j < SORT_SPT; j++) {
+    const uint32_t i = blockIdx.x * SORT_BLK + j * 256 + t;
+    const uint32_t ig = point_base + b * point_stride + i;  // SRS index of this scalar
+    if (i < n && !inf[ig]) {
+      uint32_t s[8];
+      load_scalar(scalars + b * stride_words + (size_t)i * 8, s);
+      uint32_t carry = 0;
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        int d = digit_at<CB>(s, w, carry);
+        if (d != 0) {
+          const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+#ifdef KZGX_SCATTER_DIRECT
+          const uint32_t kk = (uint32_t)((d < 0 ? -d : d) - 1);
+          entries[b * emax + bbase[hb + kk] + (pos - lstart[kk])] = ((uint32_t)w * n_srs + ig) | (d < 0 ? 0x80000000u : 0u);
+#else
+          stage[pos] = ((uint32_t)w * n_srs + ig) | (d < 0 ? 0x80000000u : 0u);
+#endif
+        }
       }
     }
   }
+  __syncthreads();
+  for (uint32_t k = t; k < NB; k += 256) cur[k] = bbase[hb + k];  // global write bases
+  __syncthreads();
+#ifdef KZGX_SCATTER_DIRECT
+  (void)stage;
+#endif
+  uint32_t* out = entries + b * emax;
+#ifdef KZGX_SCATTER_DIRECT
+  const uint32_t total = 0;
+#else
+  const uint32_t total = lstart[NB];
+#endif
+  for (uint32_t j = t; j < total; j += 256) {
+    uint32_t lo = 0, hi = NB;  // bucket of position j: lstart[lo] <= j < lstart[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lstart[mid] <= j)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    out[cur[lo] + (j - lstart[lo])] = stage[j];
+  }
 }
 
-// pass 4: balanced bucket accumulation, K entries per thread
+// pass 4: balanced bucket accumulation.  Thread s of an MSM owns the K
+// consecutive sorted entries [s K, s K + K) and runs K mixed XYZZ additions
+// from the L2-resident window table (the entry and table point of the next
+// term in flight underneath).  Buckets that start and end inside the segment
+// are written straight to bsum.  The partial of the bucket already open at the
+// segment start (its "head", sstate HEAD; SPANS if that bucket also runs past
+// the segment) and of a bucket that starts inside the segment and runs past
+// its end (its "tail", tailk = bucket) go to per-segment slots for pass 4b.
+// Keeping the merges out of this loop keeps it at 4 waves per SIMD.
 constexpr uint32_t NO_TAIL = 0xffffffffu;
+constexpr uint32_t ACC_WG = 128;  // segments per merge workgroup
+constexpr uint8_t HEAD = 1, SPANS = 2;
+
+// waves per SIMD the accumulation kernel is register-budgeted for (the
+// 14-limb BLS12-381 field spills at 3)
+template <class C>
+constexpr int pip_accum_waves() {
+  return C::Fp29::L <= 9 ? KZGX_ACCUM_WAVES : 2;
+}
 
 template <class C>
-__global__ __launch_bounds__(256, KZGX_ACCUM_WAVES) void k_msm_accum(const uint32_t* __restrict__ entries, size_t emax,
-                                                   const uint32_t* __restrict__ offsets, uint32_t nb,
-                                                   const uint32_t* __restrict__ table, uint32_t K, size_t smax,
-                                                   uint32_t* __restrict__ bsum, uint32_t* __restrict__ heads,
-                                                   uint32_t* __restrict__ tails, uint32_t* __restrict__ tailk) {
+__global__ __launch_bounds__(256, pip_accum_waves<C>()) void k_msm_accum(
+    const uint32_t* __restrict__ entries, size_t emax, const uint32_t* __restrict__ offsets, uint32_t nb,
+    const uint32_t* __restrict__ table, uint32_t K, uint32_t smax, uint32_t* __restrict__ bsum,
+    uint32_t* __restrict__ heads, uint32_t* __restrict__ tails, uint32_t* __restrict__ tailk,
+    uint8_t* __restrict__ sstate) {
   constexpr int PW = affine_words<C>();
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg >= smax) return;
+  const size_t si = (size_t)b * smax + seg;
   const uint32_t* off = offsets + (size_t)b * (nb + 1);
   const uint32_t E = off[nb];
   const uint32_t start = seg * K;
-  if (start >= E) return;
-  const uint32_t end = min(start + K, E);
-  // bucket k with off[k] <= start < off[k+1]
-  uint32_t lo = 0, hi = nb;  // invariant off[lo] <= start < off[hi]
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (off[mid] <= start)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  uint32_t k = lo;
-  uint32_t next = off[k + 1];
-  bool before = off[k] < start;
-  const uint32_t* ent = entries + b * emax;
-  Xyzz<C> acc = xyzz_inf<C>();
-  for (uint32_t p = start; p < end; ++p) {
-    if (p == next) {
-      // bucket k ended inside this segment
-      uint32_t* dst = before ? heads + ((size_t)b * smax + seg) * XW : bsum + ((size_t)b * nb + k) * XW;
-      xyzz_store<C>(dst, acc);
-      acc = xyzz_inf<C>();
-      before = false;
-      do {
-        k++;
-        next = off[k + 1];
-      } while (next == p);
-    }
-    const uint32_t e = ent[p];
-    Affine<C> a = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
-    if (e >> 31) a = affine_neg<C>(a);
-    acc = xyzz_add_affine_impl<C>(acc, a);
-  }
-  uint32_t* dst;
+  uint8_t state = 0;
   uint32_t tk = NO_TAIL;
-  if (before) {
-    dst = heads + ((size_t)b * smax + seg) * XW;
-  } else if (next > end) {
-    dst = tails + ((size_t)b * smax + seg) * XW;
-    tk = k;
-  } else {
-    dst = bsum + ((size_t)b * nb + k) * XW;
+  if (start < E) {
+    const uint32_t end = min(start + K, E);
+    // bucket k with off[k] <= start < off[k+1]
+    uint32_t lo = 0, hi = nb;  // invariant off[lo] <= start < off[hi]
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= start)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    uint32_t k = lo;
+    uint32_t next = off[k + 1];
+    bool before = off[k] < start;
+    Xyzz<C> acc = xyzz_inf<C>();
+    const uint32_t* ent = entries + b * emax;
+    // software pipeline: the entry and table point of p + 1 are in flight
+    // during the mixed addition of p (the entry of p + 2 one step earlier)
+#ifndef KZGX_NO_PREFETCH
+    uint32_t e = ent[start];
+    uint32_t e2 = start + 1 < end ? ent[start + 1] : 0u;
+    Affine<C> nx = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+#endif
+    for (uint32_t p = start; p < end; ++p) {
+#ifdef KZGX_NO_PREFETCH
+      const uint32_t e = ent[p];
+      Affine<C> a = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+      const uint32_t neg = e >> 31;
+#else
+      Affine<C> a = nx;
+      const uint32_t neg = e >> 31;
+      if (p + 1 < end) {
+        e = e2;
+        if (p + 2 < end) e2 = ent[p + 2];
+        nx = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+      }
+#endif
+      if (p == next) {  // bucket k ended inside this segment
+        if (before) {
+          xyzz_store<C>(heads + si * XW, acc);
+          state = HEAD;
+          before = false;
+        } else {
+          xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
+        }
+        acc = xyzz_inf<C>();
+        do {
+          k++;
+          next = off[k + 1];
+        } while (next == p);
+      }
+      if (neg) a = affine_neg<C>(a);
+      acc = xyzz_add_affine_impl<C>(acc, a);
+    }
+    if (before) {  // the whole segment is one head
+      xyzz_store<C>(heads + si * XW, acc);
+      state = HEAD | (next > end ? SPANS : 0);
+    } else if (next > end) {
+      xyzz_store<C>(tails + si * XW, acc);
+      tk = k;
+    } else {
+      xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
+    }
   }
-  xyzz_store<C>(dst, acc);
-  tailk[(size_t)b * smax + seg] = tk;
+  sstate[si] = state;
+  tailk[si] = tk;
 }
 
-// pass 4b: buckets that straddle segments.  The segment holding the start
-// of such a bucket stored its partial as a tail (tailk = bucket); the later
-// segments of the bucket stored heads.  One thread per segment with a tail
-// sums tail + heads into bsum, so the bucket pass below is branch-free.
+// pass 4a: merge the partials of buckets that cross segments, one workgroup
+// per ACC_WG consecutive segments with their heads staged in LDS.  A head
+// chain is the run of heads that continues one bucket: the tail's owner (or
+// thread 0, for the bucket already open at the workgroup start) adds them.
+// Short chains (the usual case: buckets shorter than K) are walked
+// sequentially; if any chain is 8 or more segments long (a skewed bucket
+// such as the top window's small digits, or a small K) the workgroup merges
+// by a segmented suffix scan over LDS in 7 steps.  The additions here are
+// calls (xyzz_add), not the inlined form: hipcc (ROCm 7.2) produced wrong
+// sums for this kernel with xyzz_add_impl inlined (bit errors in about one
+// merged bucket in ten, scripts/dbg_pippenger.py), and the merge is off the
+// hot loop.  Only buckets that cross a
+// workgroup boundary leave: its leading chain -> ghead (gflag HEAD, SPANS if
+// the bucket runs past the workgroup), its trailing tail -> gtail / gtailk,
+// merged by k_msm_wg_fixup.
 template <class C>
-__global__ __launch_bounds__(256) void k_msm_fixup(const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t K,
-                                                   size_t smax, const uint32_t* __restrict__ heads,
-                                                   const uint32_t* __restrict__ tails,
-                                                   const uint32_t* __restrict__ tailk, uint32_t* __restrict__ bsum) {
+__global__ __launch_bounds__(ACC_WG) void k_msm_merge(const uint32_t* __restrict__ heads,
+                                                      const uint32_t* __restrict__ tails,
+                                                      const uint32_t* __restrict__ tailk,
+                                                      const uint8_t* __restrict__ sstate, uint32_t smax, uint32_t nb,
+                                                      uint32_t nwg, uint32_t* __restrict__ bsum,
+                                                      uint32_t* __restrict__ ghead, uint32_t* __restrict__ gtail,
+                                                      uint32_t* __restrict__ gtailk, uint32_t* __restrict__ gflag) {
+  constexpr int XW = xyzz_words<C>();
+  __shared__ uint4 lds_head4[ACC_WG * XW / 4];
+  __shared__ uint8_t lds_state[ACC_WG];
+  __shared__ uint8_t lds_g[ACC_WG];
+  uint32_t* lds_head = reinterpret_cast<uint32_t*>(lds_head4);
+  const uint32_t b = blockIdx.y;
+  const uint32_t t = threadIdx.x;
+  const uint32_t seg = blockIdx.x * ACC_WG + t;
+  const size_t gi = (size_t)b * nwg + blockIdx.x;
+  const size_t si = (size_t)b * smax + seg;
+  uint8_t state = 0;
+  uint32_t k = NO_TAIL;
+  if (seg < smax) {
+    state = sstate[si];
+    k = tailk[si];
+  }
+  const bool has_tail = k != NO_TAIL;
+  if (state & HEAD) xyzz_store<C>(lds_head + t * XW, xyzz_load<C>(heads + si * XW));
+  lds_state[t] = state;
+  if (t == 0) gtailk[gi] = NO_TAIL;  // overwritten below by a crossing tail
+  __syncthreads();
+  // chain length (heads it sums, capped at 8) from head index u0
+  auto chain_len = [&](uint32_t u0) {
+    uint32_t c = 0;
+    for (uint32_t u = u0; u < ACC_WG && c < 8; u++) {
+      c++;
+      if (!(lds_state[u] & SPANS)) break;
+    }
+    return c;
+  };
+  bool long_chain = false;
+  if (has_tail && chain_len(t + 1) >= 8) long_chain = true;
+  if (t == 0 && (state & HEAD) && chain_len(0) >= 8) long_chain = true;
+#ifdef KZGX_MERGE_SEQ_ONLY
+  long_chain = false;
+#endif
+  if (__syncthreads_or(long_chain)) {
+    // y_u = sum of the heads u .. (chain end or workgroup end); g_u = the
+    // chain runs past the workgroup.  Step D adds y_{u+D} while the chain
+    // from u still continues past u + D - 1.
+    uint8_t g = (state & SPANS) ? 1 : 0;
+    lds_g[t] = g;
+    Xyzz<C> y = xyzz_inf<C>();
+    if (state & HEAD) y = xyzz_load<C>(lds_head + t * XW);
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t D = 1; D < ACC_WG; D <<= 1) {
+      const bool need = g && t + D < ACC_WG;
+      Xyzz<C> o;
+      uint8_t go = 0;
+      if (need) {
+        o = xyzz_load<C>(lds_head + (t + D) * XW);
+        go = lds_g[t + D];
+      }
+      __syncthreads();
+      if (need) {
+        y = xyzz_add<C>(y, o);
+        g = go;
+        xyzz_store<C>(lds_head + t * XW, y);
+        lds_g[t] = g;
+      }
+      __syncthreads();
+    }
+    if (has_tail) {
+      Xyzz<C> acc = xyzz_load<C>(tails + si * XW);
+      bool past = true;
+      if (t + 1 < ACC_WG) {
+        acc = xyzz_add<C>(acc, xyzz_load<C>(lds_head + (t + 1) * XW));
+        past = lds_g[t + 1] != 0;
+      }
+      if (!past) {
+        xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
+      } else {
+        xyzz_store<C>(gtail + gi * XW, acc);
+        gtailk[gi] = k;
+      }
+    }
+    if (t == 0) {
+      uint32_t f = 0;
+      if (state & HEAD) {
+        f = HEAD | (lds_g[0] ? SPANS : 0);
+        xyzz_store<C>(ghead + gi * XW, y);
+      }
+      gflag[gi] = f;
+    }
+    return;
+  }
+  if (has_tail) {
+    // the next segment starts inside bucket k, so it holds a head
+    Xyzz<C> acc = xyzz_load<C>(tails + si * XW);
+    uint32_t u = t + 1;
+    bool closed = false;
+    for (; u < ACC_WG; u++) {
+      acc = xyzz_add<C>(acc, xyzz_load<C>(lds_head + u * XW));
+      if (!(lds_state[u] & SPANS)) {
+        closed = true;
+        break;
+      }
+    }
+    if (closed) {
+      xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
+    } else {
+      xyzz_store<C>(gtail + gi * XW, acc);
+      gtailk[gi] = k;
+    }
+  }
+  if (t == 0) {
+    uint32_t f = 0;
+    if (state & HEAD) {
+      Xyzz<C> h = xyzz_load<C>(lds_head);
+      uint32_t u = 0;
+      f = HEAD;
+      while (lds_state[u] & SPANS) {
+        if (u + 1 == ACC_WG) {
+          f |= SPANS;
+          break;
+        }
+        u++;
+        h = xyzz_add<C>(h, xyzz_load<C>(lds_head + u * XW));
+      }
+      xyzz_store<C>(ghead + gi * XW, h);
+    }
+    gflag[gi] = f;
+  }
+}
+
+// pass 4b: buckets that cross workgroups.  The workgroup holding the start
+// of such a bucket left its partial in gtail (gtailk = bucket); the later
+// workgroups left their leading head chains in ghead.  Thread per workgroup.
+template <class C>
+__global__ __launch_bounds__(64) void k_msm_wg_fixup(uint32_t nb, uint32_t nwg, const uint32_t* __restrict__ ghead,
+                                                     const uint32_t* __restrict__ gtail,
+                                                     const uint32_t* __restrict__ gtailk,
+                                                     const uint32_t* __restrict__ gflag, uint32_t* __restrict__ bsum) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
-  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t* off = offsets + (size_t)b * (nb + 1);
-  if ((size_t)seg * K >= off[nb]) return;
-  const uint32_t k = tailk[(size_t)b * smax + seg];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nwg) return;
+  const size_t gi = (size_t)b * nwg + g;
+  const uint32_t k = gtailk[gi];
   if (k == NO_TAIL) return;
-  const uint32_t e1 = off[k + 1];
-  Xyzz<C> acc = xyzz_load<C>(tails + ((size_t)b * smax + seg) * XW);
-  for (uint32_t s = seg + 1; (size_t)s * K < e1; s++) acc = xyzz_add<C>(acc, xyzz_load<C>(heads + ((size_t)b * smax + s) * XW));
+  Xyzz<C> acc = xyzz_load<C>(gtail + gi * XW);
+  for (uint32_t h = g + 1; h < nwg; h++) {
+    const size_t hi = (size_t)b * nwg + h;
+    acc = xyzz_add<C>(acc, xyzz_load<C>(ghead + hi * XW));
+    if (!(gflag[hi] & SPANS)) break;
+  }
   xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
 }
 
-// pass 5a: finish the buckets and their first-level weighted sums.
-// Thread t of MSM b owns buckets [t J, t J + J) (J = RED_J) and emits
-//   R_t = sum_j (j+1) B_{tJ+j}   and   T_t = sum_j B_{tJ+j}
-// so that sum_k (k+1) B_k = sum_t R_t + J sum_t t T_t.
+// pass 5a: bucket running sums, J = RED_J buckets per thread.  Thread t of
+// MSM b owns buckets [t J, t J + J) and emits
+//   R_t = sum_j (j + 1) B_{tJ+j}   and   T_t = sum_j B_{tJ+j}
+// so that sum_k (k + 1) B_k = sum_t R_t + J sum_t t T_t.
 constexpr uint32_t RED_J = 8;
 
 template <class C>
@@ -312,9 +590,7 @@ __global__ __launch_bounds__(256, KZGX_BS_WAVES) void k_msm_bucket_sums(const ui
   const uint32_t* src = bsum + ((size_t)b * nb + t * RED_J) * XW;
   Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
   for (int j = (int)RED_J - 1; j >= 0; j--) {
-    Xyzz<C> bk = xyzz_inf<C>();
-    if (off[j + 1] > off[j]) bk = xyzz_load<C>(src + (size_t)j * XW);  // empty buckets were never written
-    run = xyzz_add_impl<C>(run, bk);
+    if (off[j + 1] > off[j]) run = xyzz_add_impl<C>(run, xyzz_load<C>(src + (size_t)j * XW));  // empty buckets: never written
     sum = xyzz_add_impl<C>(sum, run);
   }
   uint32_t* dst = rt + ((size_t)b * T1 + t) * 2 * XW;
@@ -322,59 +598,77 @@ __global__ __launch_bounds__(256, KZGX_BS_WAVES) void k_msm_bucket_sums(const ui
   xyzz_store<C>(dst + XW, run);
 }
 
-// pass 5b: fold the T1 (R_t, T_t) pairs of every MSM to its value
-//   V = sum_t R_t + s sum_t t T_t        (s = RED_J initially)
-// 8:1 per level: group g = {8g .. 8g+7} becomes
-//   R'_g = sum_i R_{8g+i} + s sum_i i T_{8g+i},   T'_g = sum_i T_{8g+i},
-// with s' = 8 s, which preserves V.  A 256-thread block folds 2048 / T1
-// MSMs in place in rt; at every level the live groups of all its MSMs are
-// packed onto the lowest threads so the shrinking levels occupy one
-// wavefront instead of one per MSM.  The thread of the last group converts
-// the MSM value to canonical affine (or stores the XYZZ point to xyzz_out
-// for chunked single MSMs, summed by k_xyzz_sum).
+// XYZZ point moved down the wavefront by off lanes (lanes past the end keep
+// their own value)
 template <class C>
-__global__ __launch_bounds__(256) void k_msm_fold(uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
-                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
-                                                  uint32_t* __restrict__ xyzz_out) {
+KZGX_DEV Xyzz<C> xyzz_shfl_down(const Xyzz<C>& p, int off) {
+  constexpr int L = C::Fp29::L;
+  Xyzz<C> o;
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    o.X.v[k] = __shfl_down(p.X.v[k], off, 64);
+    o.Y.v[k] = __shfl_down(p.Y.v[k], off, 64);
+    o.ZZ.v[k] = __shfl_down(p.ZZ.v[k], off, 64);
+    o.ZZZ.v[k] = __shfl_down(p.ZZZ.v[k], off, 64);
+  }
+  return o;
+}
+
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_dbl_n(Xyzz<C> p, uint32_t m) {  // 2^log2(m) p, m a power of two
+#pragma unroll 1
+  for (; m > 1; m >>= 1) p = xyzz_dbl_impl<C>(p);
+  return p;
+}
+
+// pass 5b: one wavefront per MSM folds the T1 = NB / J pairs (R_t, T_t):
+//   V = sum_t R_t + J sum_t t T_t.
+// Lane l first folds its G = T1 / 64 consecutive pairs into
+//   R'_l = sum_i R_{Gl+i} + J sum_i i T_{Gl+i},   T'_l = sum_i T_{Gl+i},
+// so V = sum_l R'_l + J G sum_l l T'_l, and sum_l l T'_l = sum_{l >= 1} S_l
+// with the suffix sums S_l = sum_{u >= l} T'_u: a 6-step __shfl_down scan.
+// U_l = R'_l + J G S_l (l >= 1) is then summed by a 6-step shuffle tree, and
+// lane 0 converts V to canonical affine (or stores the XYZZ point for
+// chunked callers, summed by k_xyzz_sum).  Four MSMs per 256-thread block.
+template <class C>
+__global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
+                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                         uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
-  const uint32_t mpb = 2048u / T1;  // MSMs per block (T1 in [64, 512])
-  const uint32_t tid = threadIdx.x;
-  uint32_t cnt = T1, stride = 1, s = RED_J;
-  while (cnt > 1) {
-    const uint32_t G = cnt >= 8 ? 8 : cnt;
-    const uint32_t groups = cnt / G;
-    if (tid < groups * mpb) {
-      const uint32_t b = blockIdx.x * mpb + tid / groups;
-      const uint32_t g = tid % groups;
-      if (b < batch) {
-        uint32_t* base = rt + ((size_t)b * T1 + (size_t)g * G * stride) * 2 * XW;
-        const size_t step = (size_t)stride * 2 * XW;
-        Xyzz<C> u = xyzz_inf<C>(), v = xyzz_inf<C>(), r = xyzz_inf<C>();
-        for (int i = (int)G - 1; i >= 1; i--) {
-          u = xyzz_add<C>(u, xyzz_load<C>(base + i * step + XW));
-          v = xyzz_add<C>(v, u);  // v = sum_i i T_i
-          r = xyzz_add<C>(r, xyzz_load<C>(base + i * step));
-        }
-        for (uint32_t m = s; m > 1; m >>= 1) v = xyzz_dbl<C>(v);
-        r = xyzz_add<C>(r, xyzz_load<C>(base));
-        const Xyzz<C> R = xyzz_add<C>(r, v);
-        if (groups > 1) {
-          xyzz_store<C>(base, R);
-          xyzz_store<C>(base + XW, xyzz_add<C>(xyzz_load<C>(base + XW), u));
-        } else if (xyzz_out) {
-          xyzz_store<C>(xyzz_out + (size_t)b * XW, R);
-        } else {
-          Affine<C> a;
-          const bool fin = xyzz_to_affine<C>(R, a);
-          affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
-          out_inf[b] = fin ? 0u : 1u;
-        }
-      }
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (b >= batch) return;  // whole wavefronts
+  const uint32_t G = T1 / 64;
+  const uint32_t* src = rt + ((size_t)b * T1 + (size_t)lane * G) * 2 * XW;
+  Xyzz<C> R = xyzz_inf<C>(), run = xyzz_inf<C>(), acc = xyzz_inf<C>();
+#pragma unroll 1
+  for (int i = (int)G - 1; i >= 1; i--) {
+    R = xyzz_add_impl<C>(R, xyzz_load<C>(src + (size_t)i * 2 * XW));
+    run = xyzz_add_impl<C>(run, xyzz_load<C>(src + (size_t)i * 2 * XW + XW));
+    acc = xyzz_add_impl<C>(acc, run);  // sum_i i T_i
+  }
+  R = xyzz_add_impl<C>(R, xyzz_load<C>(src));
+  Xyzz<C> S = xyzz_add_impl<C>(run, xyzz_load<C>(src + XW));  // T'_l
+  R = xyzz_add_impl<C>(R, xyzz_dbl_n<C>(acc, RED_J));           // R'_l
+  // inclusive suffix scan of T' over the wavefront
+#pragma unroll 1
+  for (int o = 1; o < 64; o <<= 1) {
+    const Xyzz<C> x = xyzz_shfl_down<C>(S, o);
+    if (lane + o < 64) S = xyzz_add_impl<C>(S, x);
+  }
+  Xyzz<C> U = R;
+  if (lane > 0) U = xyzz_add_impl<C>(U, xyzz_dbl_n<C>(S, RED_J * G));
+#pragma unroll 1
+  for (int o = 32; o >= 1; o >>= 1) U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, o));
+  if (lane == 0) {
+    if (xyzz_out) {
+      xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
+    } else {
+      Affine<C> a;
+      const bool fin = xyzz_to_affine<C>(U, a);
+      affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+      out_inf[b] = fin ? 0u : 1u;
     }
-    __syncthreads();
-    cnt = groups;
-    stride *= G;
-    s *= G;
   }
 }
 
@@ -428,55 +722,73 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
                    uint32_t* xyzz_out) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
-  const uint32_t K = ctx->seg_k;
   const size_t emax = (size_t)n * W;
+  // entries per accumulation thread: the context's segment length, halved
+  // (down to 8) while the grid would hold fewer than ~128k threads, so a
+  // single or small batch of MSMs still spreads over the chip
+  uint32_t K = ctx->seg_k;
+  while (K > 8 && batch * emax / K < 131072) K >>= 1;
   const size_t smax = (emax + K - 1) / K;
+  const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
+  const size_t nblk = (n + SORT_BLK - 1) / SORT_BLK;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+  if (batch > 65535 || nblk > 65535 || nwg > 65535) return KZGX_ERR_ARG;  // grid limits
   MsmWs* wsp = ctx->ws_for(st);
-  if (!wsp) return KZGX_ERR_ARG;  // too many concurrent streams on one context
+  if (!wsp) return KZGX_ERR_ARG;  // workspace binding failed (device sync error)
   MsmWs& ws = *wsp;
-  KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, batch * NB * 4, &ws.counts_b));
+  // counts: per-(MSM, count block) histograms; cursors: their write bases;
+  // heads / tails / tailk / flags: workgroup-crossing bucket partials
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, batch * nblk * NB * 4, &ws.counts_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, batch * nblk * NB * 4, &ws.cursors_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, batch * (NB + 1) * 4, &ws.offsets_b));
-  KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, batch * NB * 4, &ws.cursors_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.entries, batch * emax * 4, &ws.entries_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, batch * NB * XB, &ws.bsum_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, batch * smax * XB, &ws.heads_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, batch * smax * XB, &ws.tails_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, batch * smax * 4, &ws.tailk_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.sstate, batch * smax, &ws.sstate_b));
+  // workgroup-crossing partials: ghead / gtail points, gtailk, gflag
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.gpart, batch * nwg * 2 * XB, &ws.gpart_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.gmeta, batch * nwg * 2 * 4, &ws.gmeta_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / RED_J) * 2 * XB, &ws.rt_b));
-  KZGX_TRY_HIP(hipMemsetAsync(ws.counts, 0, batch * NB * 4, st));
+  uint32_t* ghead = ws.gpart;
+  uint32_t* gtail = ws.gpart + batch * nwg * xyzz_words<C>();
+  uint32_t* gtailk = ws.gmeta;
+  uint32_t* gflag = ws.gmeta + batch * nwg;
   dim3 blk(256);
-  dim3 gs((unsigned)((n + 255) / 256), (unsigned)batch);
+  dim3 gs((unsigned)nblk, (unsigned)batch);
   {
     ProfScope p(ctx, st, "msm_count");
     hipLaunchKernelGGL(k_msm_count<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf, ws.counts,
-                       point_base, point_stride);
+                       (uint32_t)nblk, point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_scan");
-    hipLaunchKernelGGL(k_msm_scan, dim3((unsigned)batch), blk, 0, st, ws.counts, ws.offsets, ws.cursors, NB);
+    hipLaunchKernelGGL(k_msm_scan<CB>, dim3((unsigned)batch), blk, 0, st, ws.counts, (uint32_t)nblk, ws.offsets,
+                       ws.cursors);
   }
   {
     ProfScope p(ctx, st, "msm_scatter");
     hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
-                       ws.cursors, ws.entries, emax, (uint32_t)ctx->n_srs, point_base, point_stride);
+                       ws.counts, ws.cursors, (uint32_t)nblk, ws.entries, emax, (uint32_t)ctx->n_srs, point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_accum");
-    dim3 ga((unsigned)((smax + 255) / 256), (unsigned)batch);
-    hipLaunchKernelGGL(k_msm_accum<C>, ga, blk, 0, st, ws.entries, emax, ws.offsets, NB, ctx->d_table, K, smax,
-                       ws.bsum, ws.heads, ws.tails, ws.tailk);
+    hipLaunchKernelGGL(k_msm_accum<C>, dim3((unsigned)((smax + 255) / 256), (unsigned)batch), blk, 0, st, ws.entries,
+                       emax, ws.offsets, NB, ctx->d_table, K, (uint32_t)smax, ws.bsum, ws.heads, ws.tails, ws.tailk,
+                       ws.sstate);
   }
   {
     ProfScope p(ctx, st, "msm_reduce");
-    const uint32_t T1 = NB / RED_J;
-    static_assert(NB / RED_J >= 64 && NB / RED_J <= 512, "k_msm_fold packs 2048 / T1 MSMs per block");
-    hipLaunchKernelGGL(k_msm_fixup<C>, dim3((unsigned)((smax + 255) / 256), (unsigned)batch), blk, 0, st, ws.offsets,
-                       NB, K, smax, ws.heads, ws.tails, ws.tailk, ws.bsum);
+    hipLaunchKernelGGL(k_msm_merge<C>, dim3((unsigned)nwg, (unsigned)batch), dim3(ACC_WG), 0, st, ws.heads, ws.tails,
+                       ws.tailk, ws.sstate, (uint32_t)smax, NB, (uint32_t)nwg, ws.bsum, ghead, gtail, gtailk, gflag);
+    hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg + 63) / 64), (unsigned)batch), dim3(64), 0, st, NB,
+                       (uint32_t)nwg, ghead, gtail, gtailk, gflag, ws.bsum);
+    constexpr uint32_t T1 = NB / RED_J;
+    static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
     hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
                        ws.bsum, ws.rt);
-    const uint32_t mpb = 2048u / T1;
-    hipLaunchKernelGGL(k_msm_fold<C>, dim3((unsigned)((batch + mpb - 1) / mpb)), blk, 0, st, ws.rt, T1,
+    hipLaunchKernelGGL(k_msm_bucket_fold<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
                        (uint32_t)batch, d_out, d_out_inf, xyzz_out);
   }
   KZGX_TRY_HIP(hipGetLastError());
