@@ -73,6 +73,13 @@ void init();
 void init(int curve);
 /** Curve selected by init(). */
 int curve();
+/** Extension: the GPU (HIP device ordinal) that trusted_setups constructed
+ *  after this call, and the setup-independent polynomial helpers, run on
+ *  (default 0).  One process per GPU is the multi-GPU model; a process may
+ *  also hold setups on several devices.  @throws std::invalid_argument for a
+ *  negative ordinal (a missing device fails at the next construction). */
+void set_device(int device);
+int device();
 
 class blob {
  private:

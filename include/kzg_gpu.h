@@ -167,6 +167,13 @@ int kzgx_poly_vanishing(kzgx_ctx* ctx, const uint64_t* xs, size_t n, uint64_t* z
 int kzgx_g1_validate(kzgx_ctx* ctx, const uint64_t* xy, int* ok);
 /* out = sum of count affine points (is_inf may be NULL); host pointers */
 int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t count, uint64_t* out_xy, int* out_is_inf);
+/* The same on device pointers, enqueued on stream (NULL = the context's):
+ * d_xy count canonical affine points (2 W64 words each), d_inf count uint32
+ * infinity flags (may be NULL), d_out_xy one point, d_out_inf one uint32.
+ * The fold of the sharded commit's gathered partials without a
+ * host round trip. */
+int kzgx_g1_sum_device(kzgx_ctx* ctx, const void* d_xy, const void* d_inf, size_t count, void* d_out_xy,
+                       void* d_out_inf, void* stream);
 /* One commitment sharded over several contexts, typically one per GPU (the
  * one-process form of SURVEY 8e's sharded commit; bench.py's configs[4] runs
  * the one-process-per-GPU form over RCCL).  Context k holds the SRS slice

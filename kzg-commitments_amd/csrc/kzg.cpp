@@ -20,6 +20,7 @@ namespace {
 
 int g_curve = KZGX_CURVE_BN254;
 kzgx_ctx* g_ctx = nullptr;  // default context for setup-independent poly ops
+int g_device = 0;          // kzg::set_device
 std::mutex g_mu;
 
 void check(int rc, const char* where) {
@@ -32,7 +33,7 @@ void check(int rc, const char* where) {
 
 kzgx_ctx* default_ctx() {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_ctx) check(kzgx_create(&g_ctx, g_curve, 0), "kzgx_create");
+  if (!g_ctx) check(kzgx_create(&g_ctx, g_curve, g_device), "kzgx_create");
   return g_ctx;
 }
 
@@ -233,6 +234,21 @@ void init(int curve) {
 
 int curve() { return g_curve; }
 
+void set_device(int device) {
+  if (device < 0) throw std::invalid_argument("negative device ordinal");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_ctx && device != g_device) {
+    kzgx_destroy(g_ctx);
+    g_ctx = nullptr;
+  }
+  g_device = device;
+}
+
+int device() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_device;
+}
+
 // ---- blob -------------------------------------------------------------------
 blob blob::from_string(std::string s) { return from_string(s, 0); }
 
@@ -319,7 +335,7 @@ trusted_setup::trusted_setup(int num_coeff) {
   uint8_t seed[32];
   for (auto& b : seed) b = (uint8_t)rd();
   Fr tau = Fr::from_le_bytes(seed, 32);
-  check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
+  check(kzgx_create(&ctx, g_curve, device()), "kzgx_create");
   check(kzgx_gen_srs_g1(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g1");
   check(kzgx_gen_srs_g2(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g2");
   n = (size_t)num_coeff;
@@ -329,7 +345,7 @@ trusted_setup::trusted_setup(int num_coeff) {
 
 trusted_setup::trusted_setup(int num_coeff, const Fr& tau) {
   if (num_coeff < 2) throw std::invalid_argument("num_coeff must be at least 2");
-  check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
+  check(kzgx_create(&ctx, g_curve, device()), "kzgx_create");
   check(kzgx_gen_srs_g1(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g1");
   check(kzgx_gen_srs_g2(ctx, tau.v.data(), 0, (size_t)num_coeff), "kzgx_gen_srs_g2");
   n = (size_t)num_coeff;
@@ -377,7 +393,7 @@ trusted_setup::trusted_setup(const std::string& filename) {
     get_be(&oct[1 + 2 * mb], w + 3 * nl, mb);  // y.im
     get_be(&oct[1 + 3 * mb], w + 2 * nl, mb);  // y.re
   }
-  check(kzgx_create(&ctx, g_curve, 0), "kzgx_create");
+  check(kzgx_create(&ctx, g_curve, device()), "kzgx_create");
   std::vector<int> ok(num, 0);
   check(kzgx_g2_validate(ctx, xy2.data(), num, ok.data()), "kzgx_g2_validate");
   for (uint64_t i = 0; i < num; i++)

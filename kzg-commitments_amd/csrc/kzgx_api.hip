@@ -554,6 +554,14 @@ int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t cou
   return KZGX_OK;
 }
 
+int kzgx_g1_sum_device(kzgx_ctx* ctx, const void* d_xy, const void* d_inf, size_t count, void* d_out_xy,
+                       void* d_out_inf, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (!d_out_xy || !d_out_inf || (count > 0 && !d_xy) || count > 0xffffffffu) return KZGX_ERR_ARG;
+  return kzgx::g1_sum(&ctx->c, (const uint32_t*)d_xy, (const uint32_t*)d_inf, count, (uint32_t*)d_out_xy,
+                      (uint32_t*)d_out_inf, pick(ctx, stream));
+}
+
 int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
                         size_t n, uint64_t* out_xy, int* out_is_inf) {
   if (!ctxs || !starts || nctx == 0 || (n > 0 && !scalars) || !out_xy || !out_is_inf) return KZGX_ERR_ARG;

@@ -25,7 +25,7 @@ EXPORTS = [
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
-    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum",
+    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device",
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
     "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max", "kzgx_msm_g1_sharded",
@@ -93,6 +93,7 @@ def lib():
             "kzgx_poly_vanishing": (ctypes.c_int, [vp, u64p, sz, u64p]),
             "kzgx_g1_validate": (ctypes.c_int, [vp, u64p, intp]),
             "kzgx_g1_sum": (ctypes.c_int, [vp, u64p, intp, sz, u64p, intp]),
+            "kzgx_g1_sum_device": (ctypes.c_int, [vp, vp, vp, sz, vp, vp, vp]),
             "kzgx_gen_srs_g2": (ctypes.c_int, [vp, u64p, sz, sz]),
             "kzgx_load_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_get_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
@@ -333,6 +334,11 @@ class Context:
         _chk(lib().kzgx_g1_sum(self.h, _p(pts), None if f is None else f.ctypes.data_as(intp), pts.shape[0],
                                _p(out), ctypes.byref(oi)), "kzgx_g1_sum")
         return out, bool(oi.value)
+
+    def g1_sum_device(self, d_xy: int, d_inf: int | None, count: int, d_out: int, d_out_inf: int,
+                      stream: int | None = None):
+        """Fold of count device-resident canonical points (uint32 infinity flags) on stream."""
+        _chk(lib().kzgx_g1_sum_device(self.h, d_xy, d_inf, count, d_out, d_out_inf, stream), "kzgx_g1_sum_device")
 
     # ---- verify half: G2 setup, polyeval_G2, pairing ----
     # G2 points: (n, 4 * W64) uint64 = x.re || x.im || y.re || y.im; Fp12: (12 * W64,)

@@ -61,6 +61,28 @@ def sharded_commit(n: int, world: int, rank: int, w64: int,
     return fold(pts, infs)
 
 
+def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
+                          partial_msm: Callable[[int, int], "object"],
+                          fold: Callable[["object", "object"], "object"],
+                          dist, torch) -> "object":
+    """Device-resident form of sharded_commit (bench.py's configs[4] step).
+
+    partial_msm(start, count) -> this rank's packed partial (2 W64 + 1 int64:
+    x || y || infinity flag) as a tensor on the compute device, enqueued with
+    no host synchronisation; the packed partials are all-gathered (RCCL over
+    xGMI on GPU, gloo on CPU) straight into device tensors; fold(points
+    (world, 2 W64) int64, flags (world,) int32) -> packed result tensor.
+    Nothing crosses to the host inside a step."""
+    start, count = shard_range(n, world, rank)
+    packed = partial_msm(start, count)
+    if world == 1:
+        return packed
+    outs = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(outs, packed)
+    g = torch.stack(outs)
+    return fold(g[:, : 2 * w64].contiguous(), g[:, 2 * w64].to(torch.int32).contiguous())
+
+
 def torch_all_gather(dist, device: Optional[object] = None):
     """all_gather callable over torch.distributed (RCCL on GPU, gloo on CPU)."""
     import torch

@@ -99,6 +99,12 @@ int main(int argc, char** argv) {
   const kzg::Fr tau = fr_from_hex(argv[2]);
   const std::string dir = argv[3];
 
+  // device selector (extension): explicit device 0 is the default; a
+  // negative ordinal is an argument error
+  check_test(throws([&] { kzg::set_device(-1); }), "negative device is invalid");
+  kzg::set_device(0);
+  check_test(kzg::device() == 0, "device 0 selected");
+
   // invalid_setup_test (testing.cpp:153-163)
   check_test(throws([&] { kzg::trusted_setup k(0, tau); }), "empty polynomial is invalid");
   check_test(throws([&] { kzg::trusted_setup k(1, tau); }), "0 degree polynomial is invalid");

@@ -52,6 +52,29 @@ def _worker(rank, world, port, n, results):
 
     got, _ = kzgx_dist.sharded_commit(n, world, rank, 4, partial, kzgx_dist.torch_all_gather(dist), fold)
     results[rank] = got
+
+    # the device-resident driver (bench.py's configs[4] step) on CPU tensors:
+    # packed partials, all-gather into tensors, fold over (points, int32 flags)
+    import torch
+
+    def partial_t(start, count):
+        xy, inf = partial(start, count)
+        return torch.from_numpy(kzgx_dist.pack_point(xy, inf, 4))
+
+    def fold_t(pts, flags):
+        assert pts.dtype == torch.int64 and flags.dtype == torch.int32 and pts.shape == (world, 8)
+        acc, inf = fold(pts.numpy().view(np.uint64), flags.numpy() != 0)
+        xy = np.zeros(8, dtype=np.uint64)
+        if acc is not None:
+            for j in range(4):
+                xy[j] = (acc[0] >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+                xy[4 + j] = (acc[1] >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+        return torch.from_numpy(kzgx_dist.pack_point(xy, inf, 4))
+
+    packed = kzgx_dist.sharded_commit_tensor(n, world, rank, 4, partial_t, fold_t, dist, torch)
+    xy, inf = kzgx_dist.unpack_points(packed.numpy(), 4)
+    results[("t", rank)] = None if inf[0] else (sum(int(xy[0, j]) << (64 * j) for j in range(4)),
+                                                 sum(int(xy[0, 4 + j]) << (64 * j) for j in range(4)))
     dist.destroy_process_group()
 
 
@@ -64,6 +87,7 @@ def test_sharded_commit_gloo(world):
     C = K.BN254
     exp = K.commit_via_tau(C, 0xC0FFEE, K.random_scalars(C, n, 7))
     assert all(results[r] == exp for r in range(world))
+    assert all(results[("t", r)] == exp for r in range(world))
 
 
 def test_shard_range_partitions():

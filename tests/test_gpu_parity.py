@@ -161,6 +161,35 @@ def test_g1_sum(name, C, ctx_factory, oracle_c):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
+def test_g1_sum_device(name, C, ctx_factory, oracle_c):
+    """kzgx_g1_sum_device (the sharded commit's on-device fold): device
+    points + uint32 infinity flags, enqueued on a torch stream"""
+    import torch
+    ctx = ctx_factory(name)
+    srs = oracle_c.gen_srs(name, 3, 6)
+    dev = torch.device("cuda", 0)
+    pts = torch.from_numpy(np.ascontiguousarray(srs).view(np.int64)).to(dev)
+    flags = torch.tensor([0, 1, 0, 0, 1, 0], dtype=torch.int32, device=dev)  # drop 3^1 and 3^4
+    out = torch.zeros((2 * ctx.w64,), dtype=torch.int64, device=dev)
+    oinf = torch.ones((1,), dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize(dev)
+    ctx.g1_sum_device(pts.data_ptr(), flags.data_ptr(), 6, out.data_ptr(), oinf.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    exp = K.scalar_mul(C, (C.gx, C.gy), 1 + 9 + 27 + 243)
+    assert pt(name, out.cpu().numpy().view(np.uint64), bool(oinf.item())) == exp
+    # all flagged -> infinity; no flags pointer -> plain sum
+    flags.fill_(1)
+    ctx.g1_sum_device(pts.data_ptr(), flags.data_ptr(), 6, out.data_ptr(), oinf.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    assert bool(oinf.item())
+    ctx.g1_sum_device(pts.data_ptr(), None, 6, out.data_ptr(), oinf.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    exp = K.scalar_mul(C, (C.gx, C.gy), 1 + 3 + 9 + 27 + 81 + 243)
+    assert pt(name, out.cpu().numpy().view(np.uint64), bool(oinf.item())) == exp
+
+
+@pytest.mark.parametrize("name,C", CURVES)
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 9, 64, 100, 257])
 def test_vanishing(name, C, n, ctx_factory, oracle_c):
     ctx = ctx_factory(name)
