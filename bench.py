@@ -49,8 +49,9 @@ def parse():
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
     ap.add_argument("--fixed-bits", type=int, default=-1,
-                    help="fixed-base table window (0 = Pippenger only; default 16: BN254 171.8 GB, "
-                         "BLS12-381 240.6 GB of the 288 GiB HBM)")
+                    help="fixed-base table window (0 = Pippenger only; default BN254 17: 15 windows, "
+                         "257.8 GB of 64-B entries; BLS12-381 16: 206.2 GB of 96-B entries, of the 288 GiB HBM; "
+                         "a window that does not fit steps down)")
     ap.add_argument("--fixed-ppt", type=int, default=16,
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic)")
     ap.add_argument("--table-gb", type=float, default=200.0, help="cfg5: fixed-base table budget per GPU (GB)")
@@ -99,10 +100,10 @@ def random_fr(rng, shape, r):
 
 def fixed_table_bytes(curve, c, npts):
     """device bytes of the fixed-base table (msm_fixed.hip: W x n x 2^(c-1)
-    entries of 80 B (BN254) / 112 B (BLS12-381) radix-2^29 affine points)"""
+    entries of 64 B (BN254) / 96 B (BLS12-381) packed affine points)"""
     bits = 254 if curve == "BN254" else 255
     w = (bits + 1 + c - 1) // c
-    return w * npts * (1 << (c - 1)) * (80 if curve == "BN254" else 112)
+    return w * npts * (1 << (c - 1)) * (64 if curve == "BN254" else 96)
 
 
 def set_fixed_with_fallback(kzgx, ctx, c, npts, budget=None):
@@ -283,7 +284,10 @@ def main():
                 f()
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
+    # c = 17 cuts BN254's 254-bit scalars to 15 windows (16 at c = 16: +7.8%
+    # measured on one box, profiles/r02_ab_table_layout.json); BLS12-381's
+    # 255-bit scalars need 16 windows at either width
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (17 if curve == "BN254" else 16)
 
     # ---- secondary legs on the default product path (no table): what
     # kzg::trusted_setup::create_commit / create_proof do without precompute()
@@ -397,12 +401,17 @@ def main():
         # per-launch duration, which the second stream's launch inflates
         achieved = per_step_bytes / (ms_per_step * 1e-3) / 1e9
         traffic = None
+
+        def wins_of(c):
+            return (C.r.bit_length() + 1 + c - 1) // c
+
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
         if os.path.exists(tpath):
             try:
                 with open(tpath) as f:
                     tj = json.load(f)
-                if tj.get("batch") == B and tj.get("fixed_bits") == fb[0]:
+                entry_b = fb[2] // max(1, wins_of(fb[0]) * fb[1] << (fb[0] - 1)) if fb[0] else 0
+                if tj.get("batch") == B and tj.get("fixed_bits") == fb[0] and tj.get("entry_bytes") == entry_b:
                     traffic = tj.get("msm_accum_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None

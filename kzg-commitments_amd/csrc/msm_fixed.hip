@@ -32,13 +32,18 @@
 
 namespace kzgx {
 
-// Table point layout.  KZGX_FIXED_L29 (default): x || y as radix-2^29
-// Montgomery limbs exactly as the accumulation kernel consumes them, padded
-// to 16 B (80 B BN254, 112 B BLS12-381) -- no per-term unpacking in the hot
-// loop.  Otherwise: x || y as canonical-width 32-bit words (64 B / 96 B),
-// 12-17% smaller, unpacked per term.
+// Table point layout.  Default (KZGX_FIXED_L29 = 0): x || y as canonical-
+// width 32-bit words, 64 B (BN254) / 96 B (BLS12-381), unpacked to radix-2^29
+// limbs per term.  KZGX_FIXED_L29 = 1: the radix-2^29 limbs the accumulation
+// consumes, padded to 80 B / 112 B (no unpacking).  Measured on MI355X
+// (profiles/r02_pmc_fetch_calibration.json): every DRAM read is a 128-B
+// request, an 80-B entry costs 1.5 lines and a 64-B entry exactly one, so
+// the packed layout moves 33% fewer bytes (8.7 vs 13.0 GB per 1024-MSM
+// launch) and needs 20% less HBM (137.5 vs 171.8 GB at c = 16) at the same
+// throughput: the ~36 unpack instructions per term hide under the VALU-bound
+// mixed addition.
 #ifndef KZGX_FIXED_L29
-#define KZGX_FIXED_L29 1
+#define KZGX_FIXED_L29 0
 #endif
 template <class C>
 constexpr int packed_words() {
