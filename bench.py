@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
     ap.add_argument("--fixed-bits", type=int, default=-1,
                     help="fixed-base table window (0 = Pippenger only; default BN254 17: 15 windows, "
-                         "257.8 GB of 64-B entries; BLS12-381 16: 206.2 GB of 96-B entries, of the 288 GiB HBM; "
+                         "257.8 GB of 64-B entries; BLS12-381 16: 240.6 GB of 112-B entries, of the 288 GiB HBM; "
                          "a window that does not fit steps down)")
     ap.add_argument("--fixed-ppt", type=int, default=16,
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic)")
@@ -100,10 +100,10 @@ def random_fr(rng, shape, r):
 
 def fixed_table_bytes(curve, c, npts):
     """device bytes of the fixed-base table (msm_fixed.hip: W x n x 2^(c-1)
-    entries of 64 B (BN254) / 96 B (BLS12-381) packed affine points)"""
+    entries of 64 B (BN254, packed words) / 112 B (BLS12-381, radix-2^29 limbs))"""
     bits = 254 if curve == "BN254" else 255
     w = (bits + 1 + c - 1) // c
-    return w * npts * (1 << (c - 1)) * (64 if curve == "BN254" else 96)
+    return w * npts * (1 << (c - 1)) * (64 if curve == "BN254" else 112)
 
 
 def set_fixed_with_fallback(kzgx, ctx, c, npts, budget=None):

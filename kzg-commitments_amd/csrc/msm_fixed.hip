@@ -10,8 +10,9 @@
 //
 //   M[w][i][j] = (j + 1) 2^(c w) P_i      w < W, i < n_t, j < H = 2^(c-1)
 //
-// stored affine, Montgomery form, as radix-2^29 limbs (80 B BN254 / 112 B
-// BLS12-381, see KZGX_FIXED_L29).  A scalar s_i with signed c-bit digits d_w (|d_w| <= H) then
+// stored affine, Montgomery form (64-B packed words on BN254, 112-B radix-2^29
+// limbs on BLS12-381, see fixed_l29).  A scalar s_i with signed c-bit digits
+// d_w (|d_w| <= H) then
 // contributes sum_w sign(d_w) M[w][i][|d_w| - 1], so an MSM is a plain sum
 // of n W table points: no bucket sort, no bucket reduction, no doublings.
 // Each thread sums the W terms of ~P points into one XYZZ accumulator with
@@ -19,8 +20,8 @@
 // table lookup for the next term in flight underneath), one wavefront per
 // MSM folds the partials, and one thread per MSM converts to affine.
 //
-// Size: W n_t H points; BN254 c = 16 (W = 16) for the 4097-point prefix of
-// the degree-4096 benchmark is 172 GB -- sized for the 288 GB of HBM3E.
+// Size: W n_t H points; BN254 c = 17 (W = 15) for the 4097-point prefix of
+// the degree-4096 benchmark is 257.8 GB -- sized for the 288 GB of HBM3E.
 // Every step is an exact group operation, so the affine output is bit-exact
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
@@ -32,22 +33,28 @@
 
 namespace kzgx {
 
-// Table point layout.  Default (KZGX_FIXED_L29 = 0): x || y as canonical-
-// width 32-bit words, 64 B (BN254) / 96 B (BLS12-381), unpacked to radix-2^29
-// limbs per term.  KZGX_FIXED_L29 = 1: the radix-2^29 limbs the accumulation
-// consumes, padded to 80 B / 112 B (no unpacking).  Measured on MI355X
-// (profiles/r02_pmc_fetch_calibration.json): every DRAM read is a 128-B
-// request, an 80-B entry costs 1.5 lines and a 64-B entry exactly one, so
-// the packed layout moves 33% fewer bytes (8.7 vs 13.0 GB per 1024-MSM
-// launch) and needs 20% less HBM (137.5 vs 171.8 GB at c = 16) at the same
-// throughput: the ~36 unpack instructions per term hide under the VALU-bound
-// mixed addition.
-#ifndef KZGX_FIXED_L29
-#define KZGX_FIXED_L29 0
+// Table point layout, per curve (KZGX_FIXED_L29 = 0 / 1 forces one for both):
+//  * packed: x || y as canonical-width 32-bit words, 64 B (BN254) / 96 B
+//    (BLS12-381), unpacked to radix-2^29 limbs per term;
+//  * radix-2^29: the limbs the accumulation consumes, padded to 80 B / 112 B.
+// Measured on MI355X (profiles/r02_pmc_fetch_calibration.json): every DRAM
+// read is a 128-B request; an 80-B BN254 entry costs 1.5 lines and a 64-B
+// one exactly one, so packed moves 33% fewer bytes (8.7 vs 13.0 GB per
+// 1024-MSM launch), needs 20% less HBM and is 1% faster -- and lets c = 17
+// (15 windows) fit.  BLS12-381 keeps the radix-2^29 entries: its 14-limb
+// unpack does not hide, 112-B entries are 2% faster than 96-B ones
+// (profiles/r02_ab_table_layout.json).
+template <class C>
+constexpr bool fixed_l29() {
+#ifdef KZGX_FIXED_L29
+  return KZGX_FIXED_L29 != 0;
+#else
+  return C::Fp29::L > 9;
 #endif
+}
 template <class C>
 constexpr int packed_words() {
-  return KZGX_FIXED_L29 ? affine_words<C>() : 2 * C::Fp::N;
+  return fixed_l29<C>() ? affine_words<C>() : 2 * C::Fp::N;
 }
 
 template <class C, int CB>
@@ -65,7 +72,7 @@ int fixed_windows(int curve, int c) {
 
 template <class C>
 KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
-  if (KZGX_FIXED_L29) return affine_load<C>(p);
+  if (fixed_l29<C>()) return affine_load<C>(p);
   using F = typename C::Fp29;
   constexpr int N = C::Fp::N;
   uint32_t wx[N], wy[N];
@@ -84,7 +91,7 @@ KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
 
 template <class C>
 KZGX_DEV void packed_store(uint32_t* __restrict__ p, const Affine<C>& a) {
-  if (KZGX_FIXED_L29) {
+  if (fixed_l29<C>()) {
     affine_store<C>(p, a);
     return;
   }
@@ -218,7 +225,7 @@ template <class C>
 KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
   using F = typename C::Fp29;
   Affine<C> a;
-  if (KZGX_FIXED_L29) {
+  if (fixed_l29<C>()) {
     constexpr int L = F::L;
     uint32_t w[packed_words<C>()];
 #pragma unroll
