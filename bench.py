@@ -212,10 +212,21 @@ def main():
     import torch
     import torch.distributed as dist
 
-    if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://")
+    # one process per GPU; KZGX_BENCH_ONE_DEVICE=1 maps every rank to device 0
+    # and KZGX_DIST_BACKEND=gloo swaps RCCL for gloo -- only to rehearse the
+    # N > 1 control flow on a one-GPU box (the driver's runs use neither)
+    if os.environ.get("KZGX_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        backend = os.environ.get("KZGX_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            # bind the communicator to this rank's GPU up front (barriers and
+            # collectives then never guess the device)
+            dist.init_process_group(backend="nccl", init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend, init_method="env://")
 
     import kzgx
 
