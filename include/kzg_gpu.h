@@ -87,13 +87,13 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
 
 /* fixed-base precomputation (the SRS is fixed for a trusted_setup's
  * lifetime): store M[w][i][j] = (j+1) 2^(c w) SRS[i] for the first n_points
- * SRS points, w < ceil((bits(r)+1)/c), j < 2^(c-1), packed affine
- * (2 x 32 B BN254, 2 x 48 B BLS12-381).  Every MSM with n <= n_points then
- * runs as a plain sum of table points (no bucket sort / reduction).  Built
- * now if an SRS is installed, else when one is; rebuilt on every SRS change.
- * c = 0 turns it off (Pippenger for every MSM).  c in {4, 7..17};
- * BN254 c = 16 over 4097 points takes 171.8 GB of device memory (80-B
- * radix-2^29 entries). */
+ * SRS points, w < ceil((bits(r)+1)/c), j < 2^(c-1), affine (BN254: 64-B
+ * packed words; BLS12-381: 112-B radix-2^29 limbs).  Every MSM with
+ * n <= n_points then runs as a plain sum of table points (no bucket sort /
+ * reduction).  Built now if an SRS is installed, else when one is; rebuilt
+ * on every SRS change.  c = 0 turns it off (Pippenger for every MSM).
+ * c in {4, 7..17}; BN254 c = 17 over 4097 points (15 windows) takes
+ * 257.8 GB of device memory, c = 16 137.5 GB. */
 int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
 /* built table: window bits (0 = none), points covered, device bytes */
 int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
