@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=0,
                     help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default 1024, cfg3 4096 "
                          "(BASELINE configs[2]: 4096 openings)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "common"],
+                    help="cfg2..cfg5: BASELINE.json configs[1..4]; common: benchmark.cpp --benchmark-common")
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
     ap.add_argument("--segment", type=int, default=128, help="sorted entries per accumulation thread")
     ap.add_argument("--fixed-bits", type=int, default=-1,
@@ -232,6 +233,8 @@ def main():
 
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local, dev, torch, dist, kzgx)
+    if args.workload == "common":
+        return run_common(args, world, rank, local, dev, torch, dist, kzgx)
 
     curve = "BLS12381" if args.workload == "cfg4" else "BN254"
     K, C = curve_consts(curve)
@@ -610,6 +613,81 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    ctx.close()
+
+
+def run_common(args, world, rank, local, dev, torch, dist, kzgx):
+    """benchmark/benchmark.cpp --benchmark-common (:123-136): one
+    10,429,000-point trusted setup (G1 and G2, generated on the GPU; timed as
+    setup like the reference's "Finished loading setup"), then for degree =
+    1024, 2048, ... <= 10,428,576 the timed regions of benchmark_single_proof
+    (:40-66): one create_commit, one create_proof(poly, 0, 1) and one
+    verify_proof of that opening, each through the C ABI calls the C++ facade
+    makes (host buffers in and out, median of 3).  Coefficients are seeded
+    uniform residues instead of an interpolated random string (from_blob is
+    outside the reference's timed regions).  Every commitment is checked
+    against [P(tau)]G1 (C Horner + scalar multiplication, test
+    infrastructure), every opening by verify_proof.  Rank 0 only: one GPU."""
+    K, C = curve_consts("BN254")
+    import corc  # checker only (oracle/ is on sys.path after curve_consts)
+
+    tau = K.default_tau(C)
+    n_setup = 10429000
+    ctx = kzgx.Context("BN254", device=local)
+    ctx.set_window_bits(args.window_bits)
+    t0 = time.perf_counter()
+    ctx.gen_srs(tau, n_setup)
+    ctx.gen_srs_g2(tau, n_setup)
+    ctx.sync()
+    setup_s = time.perf_counter() - t0
+    rng = np.random.default_rng(0x4B5A47)
+    rows = []
+    ok_all = True
+    degree = 1024
+    reps = 3
+    while degree <= 10428576:
+        n = degree + 1
+        P = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+        P[:, 3] &= np.uint64((1 << 59) - 1)  # < 2^251 < r
+        z0 = np.zeros((1, 4), dtype=np.uint64)
+        commit_ms = median_ms(lambda: ctx.msm(P), reps)
+        cxy, cinf = ctx.msm(P)
+        proof_ms = median_ms(lambda: ctx.prove_single_batch(P, z0), reps)
+        pxy, pinf, y = ctx.prove_single_batch(P, z0)
+        verify_ms = median_ms(lambda: ctx.verify_proof(cxy, cinf, pxy[0], bool(pinf[0]), z0, y), reps)
+        verified = ctx.verify_proof(cxy, cinf, pxy[0], bool(pinf[0]), z0, y)
+        exp = corc.scalar_mul("BN254", (C.gx, C.gy), corc.poly_eval("BN254", P, tau) % C.r)
+        got = None if cinf else (to_int(cxy[:4]), to_int(cxy[4:8]))
+        ok = verified and got == exp
+        ok_all = ok_all and ok
+        rows.append({"degree": degree, "commit_ms": commit_ms, "proof_ms": proof_ms, "verify_ms": verify_ms,
+                     "commit_ok": got == exp, "verified": verified})
+        print("common: degree %8d commit %8.3f ms proof %8.3f ms verify %7.3f ms %s" % (
+            degree, commit_ms, proof_ms, verify_ms, "ok" if ok else "MISMATCH"), file=sys.stderr, flush=True)
+        degree *= 2
+    top = rows[-1]
+    line = {
+        "metric": "KZG single commit/proof/verify latency, BN254, 10,429,000-point setup (benchmark-common)",
+        "value": 1e3 / top["commit_ms"],
+        "unit": "commits/s at degree %d" % top["degree"],
+        "n_gpus": 1,
+        "steps": reps,
+        "warmup": 1,
+        "ms_per_step": top["commit_ms"],
+        "higher_is_better": True,
+        "scaling": "none",
+        "vs_baseline": None,
+        "dtype": "uint32 limbs (254-bit Montgomery Fp)",
+        "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 / [tau^i]G2 from fixed tau",
+        "config": {"workload": "benchmark.cpp --benchmark-common: setup of 10429000 points, degree 1024..8388608",
+                   "msm": "pippenger (chunked for n >= 16384), c=%d" % args.window_bits,
+                   "host_buffers": True},
+        "secondary": {"setup_s": setup_s, "per_degree": rows},
+        "parity": {"checked": len(rows), "ok": int(sum(r["commit_ok"] and r["verified"] for r in rows)),
+                   "method": "[P(tau)]G1 identity + verify_proof"},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     ctx.close()
 
 

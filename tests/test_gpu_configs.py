@@ -267,3 +267,26 @@ def test_cfg5_commit_sharded(cfg5_poly, shards):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_benchmark_common_degree_2_23():
+    """benchmark.cpp --benchmark-common (:123-136): a 10,429,000-point setup
+    and its largest commit, degree 2^23 (8,388,609 coefficients), through the
+    table-less chunked Pippenger (2049 chunks), against [P(tau)]G1"""
+    import corc
+    import kzgx
+    C = K.BN254
+    tau = K.default_tau(C)
+    n = (1 << 23) + 1
+    rng = np.random.default_rng(0xC0)
+    S = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+    S[:, 3] &= np.uint64((1 << 59) - 1)
+    S[n // 3] = 0
+    exp = g_mul("BN254", C, corc.poly_eval("BN254", S, tau))
+    ctx = kzgx.Context("BN254")
+    try:
+        ctx.gen_srs(tau, 10429000)
+        out, inf = ctx.msm(S)
+        assert pt("BN254", out, inf) == exp
+    finally:
+        ctx.close()
