@@ -863,7 +863,10 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;
   if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
-  if (batch == 1 && n >= 4 * MSM_CHUNK)
+#ifndef KZGX_CHUNK_MIN
+#define KZGX_CHUNK_MIN (4 * MSM_CHUNK)
+#endif
+  if (batch == 1 && n >= KZGX_CHUNK_MIN)
     return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
               : msm_single_chunked<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
   return bn ? msm_batch_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr)

@@ -19,6 +19,8 @@
 // needed on the streaming paths.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <utility>
 
 #include "field.hpp"
@@ -107,6 +109,96 @@ __global__ __launch_bounds__(256) void k_quotient_single(const uint32_t* __restr
       fe_store<FR>(ys + (size_t)j * N, h);
   }
   if (n == 0 && lane == 0 && ys) fe_store<FR>(ys + (size_t)j * N, fe_zero<FR>());
+}
+
+// Large single openings (batch <= 4, n >= 2^13): the same three phases spread
+// over the whole chip instead of one wavefront.  Lane t of the grid owns
+// coefficients [t L, t L + L) (zeros past n); with h_k = sum_{i >= k} p_i z^(i-k)
+// (q_{k-1} = h_k, y = h_0):
+//   k_qbig_local : lane-local Horner, then a wavefront suffix scan with
+//                  multiplier z^L -> c_t (the wavefront-local h at t L) and
+//                  the wavefront total H_g;
+//   k_qbig_scan  : one workgroup scans the G totals with multiplier z^(64 L)
+//                  -> C_g = h at the top of wavefront g, and y;
+//   k_qbig_replay: lane carry-in c_{t+1} + z^(L (63 - l)) C_g, then the
+//                  chunk replayed, emitting q.
+template <class FR>
+__global__ __launch_bounds__(256) void k_qbig_local(const uint32_t* __restrict__ P, uint32_t n,
+                                                    const uint32_t* __restrict__ z, uint32_t L,
+                                                    uint32_t* __restrict__ cl, uint32_t* __restrict__ H) {
+  constexpr int N = FR::N;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const Fe<FR> zm = fe_to_mont<FR>(fe_load<FR>(z));
+  const uint64_t lo64 = (uint64_t)t * L;
+  const uint32_t lo = (uint32_t)(lo64 < n ? lo64 : n), hi = (uint32_t)(lo64 + L < n ? lo64 + L : n);
+  Fe<FR> h = fe_zero<FR>();
+  for (uint32_t k = hi; k-- > lo;) h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+  Fe<FR> c = h;
+  Fe<FR> zp = fe_pow_u32<FR>(zm, L);
+#pragma unroll
+  for (int s = 0; s < 6; s++) {
+    Fe<FR> o = fe_shfl_down<FR>(c, 1 << s);
+    if (lane + (1u << s) < 64) c = fe_add<FR>(c, fe_mul<FR>(o, zp));
+    zp = fe_sqr<FR>(zp);
+  }
+  fe_store<FR>(cl + (size_t)t * N, c);
+  if (lane == 0) fe_store<FR>(H + (size_t)(t >> 6) * N, c);
+}
+
+template <class FR>
+__global__ __launch_bounds__(256) void k_qbig_scan(const uint32_t* __restrict__ H, uint32_t G,
+                                                   const uint32_t* __restrict__ z, uint32_t L,
+                                                   uint32_t* __restrict__ Cg, uint32_t* __restrict__ y) {
+  constexpr int N = FR::N;
+  __shared__ uint32_t sh[256 * N];
+  const uint32_t t = threadIdx.x;
+  const Fe<FR> zm = fe_to_mont<FR>(fe_load<FR>(z));
+  const Fe<FR> Z = fe_pow_u32<FR>(zm, 64u * L);  // one wavefront's span
+  const uint32_t per = (G + 255) / 256;
+  const uint32_t g0 = min(t * per, G), g1 = min(g0 + per, G);
+  Fe<FR> u = fe_zero<FR>();
+  for (uint32_t g = g1; g-- > g0;) u = fe_add<FR>(fe_load<FR>(H + (size_t)g * N), fe_mul<FR>(u, Z));
+  // S_t = sum_{t' >= t} u_t' Z^(per (t' - t)), Hillis-Steele over LDS
+  Fe<FR> S = u;
+  Fe<FR> Zp = fe_pow_u32<FR>(Z, per);
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    fe_store<FR>(sh + t * N, S);
+    __syncthreads();
+    if (t + d < 256) S = fe_add<FR>(S, fe_mul<FR>(fe_load<FR>(sh + (t + d) * N), Zp));
+    __syncthreads();
+    Zp = fe_sqr<FR>(Zp);
+  }
+  fe_store<FR>(sh + t * N, S);
+  __syncthreads();
+  Fe<FR> K = t + 1 < 256 ? fe_load<FR>(sh + (t + 1) * N) : fe_zero<FR>();
+  // K = h at the top of this thread's range (ranges start at multiples of
+  // per; only the last non-empty one can be short, and it has no successor)
+  for (uint32_t g = g1; g-- > g0;) {
+    fe_store<FR>(Cg + (size_t)g * N, K);
+    K = fe_add<FR>(fe_load<FR>(H + (size_t)g * N), fe_mul<FR>(K, Z));
+  }
+  if (t == 0 && y) fe_store<FR>(y, K);
+}
+
+template <class FR>
+__global__ __launch_bounds__(256) void k_qbig_replay(const uint32_t* __restrict__ P, uint32_t n,
+                                                     const uint32_t* __restrict__ z, uint32_t L,
+                                                     const uint32_t* __restrict__ cl, const uint32_t* __restrict__ Cg,
+                                                     uint32_t* __restrict__ q) {
+  constexpr int N = FR::N;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lo64 = (uint64_t)t * L;
+  if (lo64 >= n) return;
+  const uint32_t lo = (uint32_t)lo64, hi = (uint32_t)(lo64 + L < n ? lo64 + L : n);
+  const Fe<FR> zm = fe_to_mont<FR>(fe_load<FR>(z));
+  Fe<FR> h = fe_mul<FR>(fe_load<FR>(Cg + (size_t)(t >> 6) * N), fe_pow_u32<FR>(zm, L * (63u - lane)));
+  if (lane < 63) h = fe_add<FR>(h, fe_load<FR>(cl + (size_t)(t + 1) * N));
+  for (uint32_t k = hi; k-- > lo;) {
+    h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+    if (k >= 1) fe_store<FR>(q + (size_t)(k - 1) * N, h);
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -270,6 +362,33 @@ static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, si
                                 uint32_t* d_q, size_t qstride, uint32_t* d_y, hipStream_t st) {
   if (batch == 0) return KZGX_OK;
   ProfScope prof(ctx, st, "quotient_single");
+  constexpr size_t QBIG_N = 1u << 13;   // from here a single opening spreads over the chip
+  constexpr size_t QBIG_LANES = 1u << 18;  // 4096 wavefronts: 4 per SIMD
+  if (batch <= 4 && n >= QBIG_N) {
+    constexpr int N = FR::N;
+    const uint32_t L = (uint32_t)std::max<size_t>(8, (n + QBIG_LANES - 1) / QBIG_LANES);
+    const size_t T = (n + L - 1) / L;
+    const size_t Tw = (T + 255) / 256 * 256;  // whole workgroups
+    const size_t G = Tw / 64;
+    MsmWs* ws = ctx->ws_for(st);
+    if (!ws) return KZGX_ERR_ARG;
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws->qbig, (Tw + 2 * G) * N * sizeof(uint32_t), &ws->qbig_b));
+    uint32_t* cl = ws->qbig;
+    uint32_t* H = cl + Tw * N;
+    uint32_t* Cg = H + G * N;
+    for (size_t j = 0; j < batch; j++) {
+      const uint32_t* P = d_coeffs + j * cstride;
+      const uint32_t* z = d_z + j * N;
+      hipLaunchKernelGGL(k_qbig_local<FR>, dim3((unsigned)(Tw / 256)), dim3(256), 0, st, P, (uint32_t)n, z, L, cl, H);
+      hipLaunchKernelGGL(k_qbig_scan<FR>, dim3(1), dim3(256), 0, st, H, (uint32_t)G, z, L, Cg,
+                         d_y ? d_y + j * N : nullptr);
+      if (n > 1)
+        hipLaunchKernelGGL(k_qbig_replay<FR>, dim3((unsigned)(Tw / 256)), dim3(256), 0, st, P, (uint32_t)n, z, L,
+                           cl, Cg, d_q + j * qstride);
+    }
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
+  }
   hipLaunchKernelGGL(k_quotient_single<FR>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, d_coeffs,
                      (uint32_t)n, cstride, d_z, (uint32_t)batch, d_q, qstride, d_y);
   KZGX_TRY_HIP(hipGetLastError());
