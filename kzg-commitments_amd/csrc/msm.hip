@@ -863,8 +863,13 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;
   if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
+// Single MSMs chunk from 2^17 points: below, one un-chunked Pippenger (the
+// segment length shrinks to spread it) has one reduction level less; above,
+// its one-workgroup scan over n / 512 count blocks serialises (measured,
+// profiles/r02_chunk_threshold.json: 65 536 points 1.31 vs 1.74 ms,
+// 2^23 points 76 vs 25 ms).
 #ifndef KZGX_CHUNK_MIN
-#define KZGX_CHUNK_MIN (4 * MSM_CHUNK)
+#define KZGX_CHUNK_MIN (32 * MSM_CHUNK)
 #endif
   if (batch == 1 && n >= KZGX_CHUNK_MIN)
     return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)

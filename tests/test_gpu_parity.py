@@ -222,9 +222,10 @@ def test_msm_window_and_segment_variants(name, C, c, seg):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-@pytest.mark.parametrize("n", [16384, 16385, 20000, 70001])
+@pytest.mark.parametrize("n", [16384, 16385, 20000, 70001, 131072, 140001])
 def test_large_single_msm_chunked(name, C, n, ctx_factory):
-    """single MSMs of >= 4 chunks run as a chunked batch + XYZZ tree sum"""
+    """single large MSMs: one Pippenger below 2^17 points (segments shrink to
+    spread it), from 2^17 a chunked batch + XYZZ tree sum"""
     ctx = ctx_factory(name)
     tau = K.default_tau(C)
     ctx.gen_srs(tau, n + 3)
