@@ -18,8 +18,8 @@
 //    inside the workgroup, only workgroup-crossing buckets go through HBM;
 //  * the bucket running sum sum_k (k+1) B_k: per-thread running sums over
 //    J = 8 buckets, then one wavefront per MSM folds the (R, T) pairs with a
-//    __shfl_down suffix scan and a shuffle-tree reduction, then converts to
-//    affine.
+//    __shfl_down suffix scan and a shuffle-tree reduction; a thread per MSM
+//    converts to affine.
 // Every step is an exact group operation, so the affine output is bit-exact
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
@@ -628,11 +628,10 @@ KZGX_DEV Xyzz<C> xyzz_dbl_n(Xyzz<C> p, uint32_t m) {  // 2^log2(m) p, m a power 
 // so V = sum_l R'_l + J G sum_l l T'_l, and sum_l l T'_l = sum_{l >= 1} S_l
 // with the suffix sums S_l = sum_{u >= l} T'_u: a 6-step __shfl_down scan.
 // U_l = R'_l + J G S_l (l >= 1) is then summed by a 6-step shuffle tree, and
-// lane 0 converts V to canonical affine (or stores the XYZZ point for
-// chunked callers, summed by k_xyzz_sum).  Four MSMs per 256-thread block.
+// lane 0 stores V as an XYZZ point (k_msm_finish converts it, or chunked
+// callers sum it with k_xyzz_sum).  Four MSMs per 256-thread block.
 template <class C>
 __global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
-                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
                                                          uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -660,16 +659,21 @@ __global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restr
   if (lane > 0) U = xyzz_add_impl<C>(U, xyzz_dbl_n<C>(S, RED_J * G));
 #pragma unroll 1
   for (int o = 32; o >= 1; o >>= 1) U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, o));
-  if (lane == 0) {
-    if (xyzz_out) {
-      xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
-    } else {
-      Affine<C> a;
-      const bool fin = xyzz_to_affine<C>(U, a);
-      affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
-      out_inf[b] = fin ? 0u : 1u;
-    }
-  }
+  if (lane == 0) xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
+}
+
+// pass 6: thread per MSM, XYZZ -> canonical affine (one inversion each), off
+// the fold's single-lane critical path
+template <class C>
+__global__ __launch_bounds__(64) void k_msm_finish(const uint32_t* __restrict__ v, uint32_t batch,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  Affine<C> a;
+  const bool fin = xyzz_to_affine<C>(xyzz_load<C>(v + (size_t)b * XW), a);
+  affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+  out_inf[b] = fin ? 0u : 1u;
 }
 
 // sum of count XYZZ points -> canonical affine (one 256-thread workgroup:
@@ -788,8 +792,14 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
     hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
                        ws.bsum, ws.rt);
+    // the fold's XYZZ results go to xyzz_out (chunked callers) or to the
+    // start of bsum, which the fold no longer reads
+    uint32_t* vx = xyzz_out ? xyzz_out : ws.bsum;
     hipLaunchKernelGGL(k_msm_bucket_fold<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
-                       (uint32_t)batch, d_out, d_out_inf, xyzz_out);
+                       (uint32_t)batch, vx);
+    if (!xyzz_out)
+      hipLaunchKernelGGL(k_msm_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, vx, (uint32_t)batch,
+                         d_out, d_out_inf);
   }
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
