@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0,
-                    help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default 1024, cfg3 4096 "
-                         "(BASELINE configs[2]: 4096 openings)")
+                    help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default cfg2 2048, "
+                         "cfg4 1024, cfg3 4096 (BASELINE configs[2]: 4096 openings)")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "common"],
                     help="cfg2..cfg5: BASELINE.json configs[1..4]; common: benchmark.cpp --benchmark-common")
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
@@ -53,8 +53,9 @@ def parse():
                     help="fixed-base table window (0 = Pippenger only; default BN254 17: 15 windows, "
                          "257.8 GB of 64-B entries; BLS12-381 16: 240.6 GB of 112-B entries, of the 288 GiB HBM; "
                          "a window that does not fit steps down)")
-    ap.add_argument("--fixed-ppt", type=int, default=16,
-                    help="SRS points per accumulation thread (fixed-base path; 0 = automatic)")
+    ap.add_argument("--fixed-ppt", type=int, default=-1,
+                    help="SRS points per accumulation thread (fixed-base path; 0 = automatic; default cfg2 22: "
+                         "2048 MSMs x 3 wavefronts = two full residencies per launch, else 16)")
     ap.add_argument("--table-gb", type=float, default=200.0, help="cfg5: fixed-base table budget per GPU (GB)")
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
@@ -241,7 +242,12 @@ def main():
     tau = K.default_tau(C)
     degree = 4096
     n = degree + 1
-    B = args.batch or (4096 if args.workload == "cfg3" else 1024)
+    # cfg2: 2048 polynomials x 22 points per thread (3 wavefronts per MSM, two
+    # full residencies of the chip per launch): +2.9% over 1024 x 16 on one
+    # box, interleaved (profiles/r02_ab_table_layout.json)
+    B = args.batch or {"cfg3": 4096, "cfg2": 2048}.get(args.workload, 1024)
+    if args.fixed_ppt < 0:
+        args.fixed_ppt = 22 if args.workload == "cfg2" else 16
     ctx = kzgx.Context(curve, device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
