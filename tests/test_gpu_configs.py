@@ -290,3 +290,36 @@ def test_benchmark_common_degree_2_23():
         assert pt("BN254", out, inf) == exp
     finally:
         ctx.close()
+
+
+def test_more_streams_than_workspaces():
+    """a context keeps workspaces for 8 streams; a 9th..12th distinct stream
+    rebinds the least recently bound one after a device synchronisation
+    (kzg_gpu.h) -- results stay exact, calls never fail"""
+    import torch
+    import kzgx
+    C = K.BN254
+    tau = K.default_tau(C)
+    ctx = kzgx.Context("BN254")
+    try:
+        n, B = 257, 3
+        ctx.gen_srs(tau, n + 1)
+        dev = torch.device("cuda", 0)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(12)]
+        polys = [K.random_scalars(C, n, seed=900 + s) for s in range(len(streams))]
+        d_c = [torch.from_numpy(np.concatenate([limbs(p)] * B).view(np.int64)).to(dev) for p in polys]
+        outs = [torch.zeros((B, 8), dtype=torch.int64, device=dev) for _ in streams]
+        infs = [torch.zeros((B,), dtype=torch.int32, device=dev) for _ in streams]
+        torch.cuda.synchronize(dev)
+        for rep in range(2):
+            for s, st in enumerate(streams):
+                ctx.msm_batch_device(d_c[s].data_ptr(), n, B, n, outs[s].data_ptr(), infs[s].data_ptr(),
+                                     st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        for s in range(len(streams)):
+            exp = K.commit_via_tau(C, tau, polys[s])
+            o = outs[s].cpu().numpy().view(np.uint64)
+            for b in range(B):
+                assert pt("BN254", o[b], bool(infs[s][b].item())) == exp
+    finally:
+        ctx.close()
