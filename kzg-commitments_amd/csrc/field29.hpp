@@ -349,24 +349,46 @@ KZGX_DEV void f29_to_words(const F29<F>& a, uint32_t (&w)[NW]) {
   }
 }
 
-// a^(m-2), 4-bit fixed window over the 32-bit exponent words PM2 (NW words)
+// a^(m-2), left-to-right sliding window of width 3 over the exponent words
+// PM2 (NW 32-bit words): 4 odd powers a, a^3, a^5, a^7 (36 VGPRs on BN254;
+// a 16-entry fixed window spilled to scratch on the latency-bound paths that
+// use this, k_*_finish and k_xyzz_sum), ~254 squarings + ~64 products.
 template <class F, int NW>
 __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW]) {
-  F29<F> tbl[16];
-  tbl[0] = f29_one<F>();
-  tbl[1] = a;
+  F29<F> odd[4];
+  odd[0] = a;
+  const F29<F> a2 = f29_sqr<F>(a);
 #pragma unroll
-  for (int i = 2; i < 16; i++) tbl[i] = f29_mul<F>(tbl[i - 1], a);
-  F29<F> acc = f29_one<F>();
-  for (int nib = 8 * NW - 1; nib >= 0; nib--) {
+  for (int i = 1; i < 4; i++) odd[i] = f29_mul<F>(odd[i - 1], a2);
+  auto bit = [&](int i) -> uint32_t { return (pm2[i >> 5] >> (i & 31)) & 1u; };
+  // the window [i .. j] (j >= i - 2, ending in a set bit) as an odd value < 8
+  auto window = [&](int i, int& j) -> F29<F> {
+    j = i - 2 < 0 ? 0 : i - 2;
+    while (!bit(j)) j++;
+    uint32_t w = 0;
+    for (int k = i; k >= j; k--) w = (w << 1) | bit(k);
+    const int idx = (int)(w >> 1);
+    F29<F> m = odd[0];
 #pragma unroll
-    for (int s = 0; s < 4; s++) acc = f29_sqr<F>(acc);
-    const uint32_t d = (pm2[nib >> 3] >> (4 * (nib & 7))) & 15u;
-    F29<F> m = tbl[0];
-#pragma unroll
-    for (int k = 1; k < 16; k++)
-      if (k == (int)d) m = tbl[k];
+    for (int k = 1; k < 4; k++)
+      if (k == idx) m = odd[k];
+    return m;
+  };
+  int i = 32 * NW - 1;
+  while (i >= 0 && !bit(i)) i--;
+  int j = 0;
+  F29<F> acc = window(i, j);  // m - 2 > 0: the top window exists
+  i = j - 1;
+  while (i >= 0) {
+    if (!bit(i)) {
+      acc = f29_sqr<F>(acc);
+      i--;
+      continue;
+    }
+    const F29<F> m = window(i, j);
+    for (int k = i; k >= j; k--) acc = f29_sqr<F>(acc);
     acc = f29_mul<F>(acc, m);
+    i = j - 1;
   }
   return acc;
 }

@@ -685,12 +685,12 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
   extern __shared__ uint32_t lds[];
   const uint32_t t = threadIdx.x;
   Xyzz<C> acc = xyzz_inf<C>();
-  for (uint32_t i = t; i < count; i += blockDim.x) acc = xyzz_add<C>(acc, xyzz_load<C>(pts + (size_t)i * XW));
+  for (uint32_t i = t; i < count; i += blockDim.x) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(pts + (size_t)i * XW));
   xyzz_store<C>(lds + t * XW, acc);
   __syncthreads();
   for (uint32_t h = blockDim.x / 2; h >= 1; h >>= 1) {
     if (t < h) {
-      acc = xyzz_add<C>(acc, xyzz_load<C>(lds + (t + h) * XW));
+      acc = xyzz_add_impl<C>(acc, xyzz_load<C>(lds + (t + h) * XW));
       xyzz_store<C>(lds + t * XW, acc);
     }
     __syncthreads();

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void k_fixed_reduce(const uint32_t* __restrict
   const uint32_t lane = threadIdx.x & 63;
   if (b >= batch) return;  // whole wavefronts
   Xyzz<C> acc = xyzz_inf<C>();
-  for (uint32_t k = lane; k < T; k += 64) acc = xyzz_add<C>(acc, xyzz_load<C>(part + ((size_t)b * T + k) * XW));
+  for (uint32_t k = lane; k < T; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(part + ((size_t)b * T + k) * XW));
   for (int off = 32; off >= 1; off >>= 1) {
     Xyzz<C> o;
 #pragma unroll
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void k_fixed_reduce(const uint32_t* __restrict
       o.ZZ.v[k] = __shfl_down(acc.ZZ.v[k], off, 64);
       o.ZZZ.v[k] = __shfl_down(acc.ZZZ.v[k], off, 64);
     }
-    acc = xyzz_add<C>(acc, o);
+    acc = xyzz_add_impl<C>(acc, o);
   }
   if (lane == 0) xyzz_store<C>(sums + (size_t)b * XW, acc);
 }
@@ -457,11 +457,14 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   uint32_t P0 = ft.pts_per_thread;
   if (P0 == 0) P0 = batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
   uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
-  // few large MSMs: two wavefront folds (64:1 each) and one workgroup sum
-  // instead of one wavefront per MSM summing T partials; T is padded to a
-  // multiple of 64^2 (the extra threads own no points: identity partials)
+  // few large MSMs: 64:1 wavefront folds until at most 128 partials per MSM
+  // remain, then one wavefront per MSM folds those and a thread per MSM
+  // converts -- instead of one wavefront per MSM summing T partials in
+  // sequence.  Beyond 64 x 128 partials T is padded to a multiple of 64^2
+  // (the extra threads own no points: identity partials) for a second 64:1
+  // level.
   const bool wave_red = batch <= 16 && T > 1024 && !xyzz_out;
-  if (wave_red) T = (T + 4095) / 4096 * 4096;
+  if (wave_red && T > 64 * 128) T = (T + 4095) / 4096 * 4096;
   MsmWs* wsp = ctx->ws_for(st);
   if (!wsp) return KZGX_ERR_ARG;
   MsmWs& ws = *wsp;
@@ -474,14 +477,27 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   }
   if (wave_red) {
     ProfScope p(ctx, st, "msm_reduce");
-    const size_t g1 = batch * (T / 64), g2 = batch * (T / 4096);
+    // level 1: 64:1 into fsum (T / 64 per MSM)
+    const size_t g1 = batch * (T / 64);
     hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g1 + 3) / 4)), dim3(256), 0, st, ws.fpart, 64u,
                        (uint32_t)g1, ws.fsum);
-    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g2 + 3) / 4)), dim3(256), 0, st, ws.fsum, 64u,
-                       (uint32_t)g2, ws.fpart);
-    const size_t xw = xyzz_words<C>(), pw = 2 * C::Fp::N;
-    for (size_t b = 0; b < batch; b++)
-      KZGX_TRY(xyzz_sum(ctx, ws.fpart + b * (T / 4096) * xw, T / 4096, d_out + b * pw, d_out_inf + b, st));
+    const uint32_t* lvl = ws.fsum;
+    size_t per = T / 64;
+    if (per > 128) {  // level 2: 64:1 back into fpart (T is a multiple of 64^2 here)
+      const size_t g2 = batch * (T / 4096);
+      hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g2 + 3) / 4)), dim3(256), 0, st, ws.fsum, 64u,
+                         (uint32_t)g2, ws.fpart);
+      lvl = ws.fpart;
+      per = T / 4096;
+    }
+    // last level: one wavefront per MSM over its `per` partials, into the
+    // buffer the last level did not read, then a thread per MSM converts
+    uint32_t* fin = lvl == ws.fsum ? ws.fpart : ws.fsum;
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, lvl, (uint32_t)per,
+                       (uint32_t)batch, fin);
+    hipLaunchKernelGGL(k_fixed_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, fin,
+                       (uint32_t)batch, d_out, d_out_inf, nullptr);
+    KZGX_TRY_HIP(hipGetLastError());
     return KZGX_OK;
   }
   {
