@@ -205,7 +205,7 @@ KZGX_DEV bool xyzz_to_affine_impl(const Xyzz<C>& p, Affine<C>& out) {
     return false;
   }
   F29<F> t = f29_mul<F>(p.ZZ, p.ZZZ);
-  F29<F> i = f29_inv<F, C::Fp::N>(t, C::Fp::PM2);  // 1 / (ZZ ZZZ)
+  F29<F> i = f29_inv_fast<F, C::Fp::N>(t, C::Fp::P, C::Fp::PM2);  // 1 / (ZZ ZZZ)
   F29<F> izz = f29_mul<F>(i, p.ZZZ);               // 1 / ZZ
   F29<F> izzz = f29_mul<F>(i, p.ZZ);               // 1 / ZZZ
   out.x = f29_reduce<F>(f29_mul<F>(p.X, izz));

@@ -93,12 +93,20 @@ KZGX_DEV F29<F> f29_sub(const F29<F>& a, const F29<F>& b, const uint32_t (&K)[F:
   return r;
 }
 
-// Modulus limb j as an opaque uniform value.  Left as a literal, a limb that
-// is a power of two (BN254: 2^25) is strength-reduced to a 64-bit shift plus
-// a 64-bit add -- two VALU issues where v_mad_u64_u32 with an SGPR operand
-// is one.  The asm is pure (not volatile), so it is hoisted out of loops.
+// Modulus limb j as an opaque uniform value (BN254).  Left as a literal, a
+// limb that is a power of two (BN254: 2^25) is strength-reduced to a 64-bit
+// shift plus a 64-bit add -- two VALU issues where v_mad_u64_u32 with an SGPR
+// operand is one.  The asm is pure (not volatile), so it is hoisted out of
+// loops.
 template <class F>
 KZGX_DEV uint32_t f29_pl(int j) {
+#ifndef KZGX_SGPR_PL_ALL
+  // BLS12-381 (14 limbs): pinning its limbs in SGPRs spills SGPRs to
+  // scratch in every point-addition kernel (111 SGPR spills, 172 B/lane of
+  // scratch in the mixed-add loop, -Rpass-analysis=kernel-resource-usage);
+  // left as literals they cost no scratch
+  if (F::L > 9) return F::P[j];
+#endif
   uint32_t r;
   asm("" : "=s"(r) : "0"(F::P[j]));
   return r;
@@ -358,8 +366,9 @@ __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW
   F29<F> odd[4];
   odd[0] = a;
   const F29<F> a2 = f29_sqr<F>(a);
-#pragma unroll
-  for (int i = 1; i < 4; i++) odd[i] = f29_mul<F>(odd[i - 1], a2);
+  odd[1] = f29_mul<F>(odd[0], a2);
+  odd[2] = f29_mul<F>(odd[1], a2);
+  odd[3] = f29_mul<F>(odd[2], a2);
   auto bit = [&](int i) -> uint32_t { return (pm2[i >> 5] >> (i & 31)) & 1u; };
   // the window [i .. j] (j >= i - 2, ending in a set bit) as an odd value < 8
   auto window = [&](int i, int& j) -> F29<F> {
@@ -391,6 +400,170 @@ __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW
     i = j - 1;
   }
   return acc;
+}
+
+// a^-1 for a Montgomery-form a < 16 m (0 -> 0): binary GCD with 60-bit
+// approximations (Pornin, "Optimized Binary GCD for Modular Inversion",
+// 2020, algorithm 2, k = 30).  Variable time: every value these paths invert
+// (commitment / proof coordinates, pairing values) is public.
+//
+// Why: on the single-MSM tails this runs in ONE lane, where every dependent
+// VALU instruction costs ~8 core clocks (scripts/lat_micro.py: a BN254
+// Montgomery product is ~2000 clocks, the Fermat chain ~417 000).  Here the
+// bit-serial work runs on two 60-bit words (the low 29 and the top 31 bits of
+// the operands) and the full-width limbs are touched once per 29 steps.
+//
+// State, in radix-2^29 limbs: y = the canonical Montgomery representative,
+// a = y, b = m, u = 1, v = 0, keeping a = u y and b = v y (mod m).  Each pass
+// runs 29 binary-GCD steps on the approximations, collecting the signed
+// matrix (f0 g0; f1 g1) (|f| + |g| <= 2^29), then
+//   a <- |a f0 + b g0| / 2^29, b <- |a f1 + b g1| / 2^29 (exact divisions),
+//   u <- (u f0 + v g0) / 2^29 mod m, v <- (u f1 + v g1) / 2^29 mod m
+// (signs folded into f, g; the mod-m halvings are Montgomery steps with
+// INV = -m^-1 mod 2^29), until a = 0; then b = 1 and v = y^-1.  BN254:
+// 13 passes on average (16 at most over 3000 random inputs), BLS12-381 19
+// (21).  The Montgomery form of the result, (y / R)^-1 R = v R^2, is two
+// products by R^2 mod m.
+template <class F, int NW>
+__device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in, const uint32_t (&)[NW]) {
+  constexpr int L = F::L;
+  constexpr int K = 29;
+  F29<F> a = f29_reduce<F>(in), b = f29_const<F>(F::P), u = f29_zero<F>(), v = f29_zero<F>();
+  if (f29_is_zero_exact<F>(a)) return a;
+  u.v[0] = 1;
+  auto approx = [](const F29<F>& x, int i, int o) -> uint64_t {
+    // bits [29 i + o, 29 i + o + 31) of x, over limbs i, i + 1, i + 2
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      w0 = j == i ? x.v[j] : w0;
+      w1 = j == i + 1 ? x.v[j] : w1;
+      w2 = j == i + 2 ? x.v[j] : w2;
+    }
+    const uint64_t w = (uint64_t)w0 | ((uint64_t)w1 << 29) | ((uint64_t)w2 << 58);
+    return (((w >> o) & 0x7fffffffull) << K) | x.v[0];
+  };
+  // (x f + y g) / 2^29 as signed limbs (the low 29 bits of the sum are zero);
+  // returns the sign and leaves |.| in r
+  auto combine = [](const F29<F>& x, const F29<F>& y, int32_t f, int32_t g, F29<F>& r) -> bool {
+    int64_t c = (int64_t)(int32_t)x.v[0] * f + (int64_t)(int32_t)y.v[0] * g;
+    c >>= K;
+#pragma unroll
+    for (int j = 1; j < L; j++) {
+      c += (int64_t)(int32_t)x.v[j] * f + (int64_t)(int32_t)y.v[j] * g;
+      r.v[j - 1] = (uint32_t)c & M29;
+      c >>= K;
+    }
+    r.v[L - 1] = (uint32_t)c;
+    const bool neg = c < 0;
+    if (neg) {  // r <- -r
+      int64_t d = 0;
+#pragma unroll
+      for (int j = 0; j < L; j++) {
+        d -= (int64_t)(int32_t)r.v[j];
+        r.v[j] = j + 1 < L ? (uint32_t)d & M29 : (uint32_t)d;
+        d >>= K;
+      }
+    }
+    return neg;
+  };
+  // (x f + y g) / 2^29 mod m, x, y in [0, m): Montgomery halving, result in
+  // (-m, 2m), then brought to [0, m)
+  auto combine_mod = [](const F29<F>& x, const F29<F>& y, int32_t f, int32_t g) -> F29<F> {
+    F29<F> r;
+    int64_t c = (int64_t)(int32_t)x.v[0] * f + (int64_t)(int32_t)y.v[0] * g;
+    const uint32_t q = ((uint32_t)c * F::INV) & M29;
+    c += (int64_t)q * F::P[0];
+    c >>= K;
+#pragma unroll
+    for (int j = 1; j < L; j++) {
+      c += (int64_t)(int32_t)x.v[j] * f + (int64_t)(int32_t)y.v[j] * g + (int64_t)q * F::P[j];
+      r.v[j - 1] = (uint32_t)c & M29;
+      c >>= K;
+    }
+    r.v[L - 1] = (uint32_t)c;
+    const uint32_t mask = c < 0 ? M29 : 0u;  // negative: + m
+    int64_t d = 0;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      d += (int64_t)(int32_t)r.v[j] + (F::P[j] & mask);
+      r.v[j] = j + 1 < L ? (uint32_t)d & M29 : (uint32_t)d;
+      d >>= K;
+    }
+    return f29_csub<F>(r, F::P);
+  };
+  // 3x the most passes seen: a bound every lane reaches even on a bad input
+  for (int pass = 0; pass < 3 * (2 * 29 * L / K + 2) && !f29_is_zero_exact<F>(a); pass++) {
+    // n = max(len(a), len(b), 60); the approximations keep bits [0, 29) and
+    // [n - 31, n)
+    uint32_t top = 0;
+    int h = 0;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const uint32_t o = a.v[j] | b.v[j];
+      h = o ? j : h;
+      top = o ? o : top;
+    }
+    int n = 29 * h + 32 - __clz(top);
+    n = n < 60 ? 60 : n;
+    const int p = n - 31, i = p / 29, o = p - 29 * i;
+    uint64_t ab = approx(a, i, o), bb = approx(b, i, o);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    int rem = K;
+    while (rem > 0) {
+      if (ab & 1) {
+        if (ab < bb) {
+          const uint64_t t = ab;
+          ab = bb;
+          bb = t;
+          int32_t s = f0;
+          f0 = f1;
+          f1 = s;
+          s = g0;
+          g0 = g1;
+          g1 = s;
+        }
+        ab -= bb;
+        f0 -= f1;
+        g0 -= g1;
+      }
+      int z = ab ? __builtin_ctzll(ab) : rem;
+      z = z < rem ? z : rem;
+      ab >>= z;
+      f1 = (int32_t)((uint32_t)f1 << z);
+      g1 = (int32_t)((uint32_t)g1 << z);
+      rem -= z;
+    }
+    F29<F> a2, b2;
+    if (combine(a, b, f0, g0, a2)) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (combine(a, b, f1, g1, b2)) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    const F29<F> u2 = combine_mod(u, v, f0, g0);
+    v = combine_mod(u, v, f1, g1);
+    u = u2;
+    a = a2;
+    b = b2;
+  }
+  const F29<F> r2 = f29_const<F>(F::R2);
+  return f29_mul<F>(f29_mul<F>(v, r2), r2);
+}
+
+// the inversion the finish / pairing paths use (KZGX_INV_FERMAT: the
+// constant-time exponentiation, for A/B runs)
+template <class F, int NW>
+KZGX_DEV F29<F> f29_inv_fast(const F29<F>& a, const uint32_t (&m)[NW], const uint32_t (&pm2)[NW]) {
+#ifdef KZGX_INV_FERMAT
+  (void)m;
+  return f29_inv<F, NW>(a, pm2);
+#else
+  (void)pm2;
+  return f29_inv_vt<F, NW>(a, m);
+#endif
 }
 
 template <class F>

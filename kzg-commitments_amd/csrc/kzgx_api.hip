@@ -902,3 +902,12 @@ extern "C" int kzgx_debug_ws_read(kzgx_ctx* ctx, const char* name, void* host, s
   KZGX_TRY_HIP(hipMemcpy(host, src, bytes, hipMemcpyDeviceToHost));
   return KZGX_OK;
 }
+
+// debug: single-lane dependent-chain latency of one primitive (msm_fixed.hip
+// k_debug_latency); res[0] = ns per operation, res[1] = core clocks
+extern "C" int kzgx_debug_latency(kzgx_ctx* ctx, int op, unsigned iters, double* res) {
+  KZGX_TRY(activate(ctx));
+  if (!res) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return kzgx::debug_latency(&ctx->c, op, iters, res);
+}

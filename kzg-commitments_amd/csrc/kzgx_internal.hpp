@@ -155,6 +155,7 @@ int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
 // mixed additions / s of the fixed-base accumulation loop on L1-resident operands (msm_fixed.hip)
 int microbench_mixed_add(Ctx* ctx, double* rate);
+int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res);  // ns, core clocks per op
 // one workgroup sums count XYZZ points -> canonical affine (msm.hip)
 int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,

@@ -23,6 +23,7 @@
 // Every step is an exact group operation, so the affine output is bit-exact
 // with any other correct evaluation of sum c_i [tau^i]G1.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "curve.hpp"
 #include "kzgx_internal.hpp"
@@ -662,6 +663,72 @@ __global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restr
   if (lane == 0) xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
 }
 
+// pass 5b, workgroup form: one 256-thread workgroup per MSM folds the T1
+// pairs, G = T1 / 256 per lane, with the same algebra as k_msm_bucket_fold:
+//   V = sum_l R'_l + J G sum_{l >= 1} S_l,  S_l = sum_{u >= l} T'_u
+// over l = 0..255.  The suffix scan is a wavefront scan plus the totals of
+// the higher wavefronts (LDS), the final sum a wavefront tree plus the four
+// wavefront sums.  Dependent chain: 3 (G - 1) + 2 + 6 + 3 + log2(J G)
+// doublings + 1 + 6 + 2 additions, against 3 (G' - 1) + 2 + log2(J) + 1 + 6
+// + log2(J G') + 1 + 6 (G' = T1 / 64) in the one-wavefront fold, and four
+// wavefronts per MSM instead of one (a batch of 1024 MSMs keeps 4 waves per
+// SIMD busy, not 1).  With out != nullptr lane 0 also converts to affine (no
+// separate finish launch).
+constexpr int FOLD_WG = 256;
+
+template <class C>
+__global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* __restrict__ rt, uint32_t T1,
+                                                                uint32_t* __restrict__ xyzz_out,
+                                                                uint32_t* __restrict__ out,
+                                                                uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  __shared__ uint32_t lds[4 * XW];
+  const uint32_t b = blockIdx.x;
+  const uint32_t l = threadIdx.x, lane = l & 63, wv = l >> 6;
+  const uint32_t G = T1 / FOLD_WG;
+  const uint32_t* src = rt + ((size_t)b * T1 + (size_t)l * G) * 2 * XW;
+  Xyzz<C> R = xyzz_load<C>(src + (size_t)(G - 1) * 2 * XW);
+  Xyzz<C> run = xyzz_load<C>(src + (size_t)(G - 1) * 2 * XW + XW);
+  Xyzz<C> acc = xyzz_inf<C>();
+#pragma unroll 1
+  for (int i = (int)G - 2; i >= 0; i--) {
+    acc = xyzz_add_impl<C>(acc, run);  // sum_i i T_i, one term per step
+    R = xyzz_add_impl<C>(R, xyzz_load<C>(src + (size_t)i * 2 * XW));
+    run = xyzz_add_impl<C>(run, xyzz_load<C>(src + (size_t)i * 2 * XW + XW));
+  }
+  if (G > 1) R = xyzz_add_impl<C>(R, xyzz_dbl_n<C>(acc, RED_J));  // R'_l
+  Xyzz<C> S = run;                                                // T'_l
+  // inclusive suffix scan of T' within the wavefront
+#pragma unroll 1
+  for (int o = 1; o < 64; o <<= 1) {
+    const Xyzz<C> x = xyzz_shfl_down<C>(S, o);
+    if (lane + o < 64) S = xyzz_add_impl<C>(S, x);
+  }
+  // + the totals of the higher wavefronts
+  if (lane == 0) xyzz_store<C>(lds + wv * XW, S);
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t w = wv + 1; w < 4; w++) S = xyzz_add_impl<C>(S, xyzz_load<C>(lds + w * XW));
+  __syncthreads();  // lds is reused below
+  Xyzz<C> U = R;
+  if (l > 0) U = xyzz_add_impl<C>(U, xyzz_dbl_n<C>(S, RED_J * G));
+#pragma unroll 1
+  for (int o = 32; o >= 1; o >>= 1) U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, o));
+  if (lane == 0) xyzz_store<C>(lds + wv * XW, U);
+  __syncthreads();
+  if (l < 2) U = xyzz_add_impl<C>(xyzz_load<C>(lds + l * XW), xyzz_load<C>(lds + (l + 2) * XW));
+  U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, 1));
+  if (l != 0) return;
+  if (xyzz_out) {
+    xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
+    return;
+  }
+  Affine<C> a;
+  const bool fin = xyzz_to_affine<C>(U, a);
+  affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+  out_inf[b] = fin ? 0u : 1u;
+}
+
 // pass 6: thread per MSM, XYZZ -> canonical affine (one inversion each), off
 // the fold's single-lane critical path
 template <class C>
@@ -792,6 +859,13 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
     hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
                        ws.bsum, ws.rt);
+    static const bool fold_wave = std::getenv("KZGX_PIP_WAVE_FOLD") != nullptr;  // A/B: the one-wavefront fold
+    if (T1 % FOLD_WG == 0 && !fold_wave) {
+      hipLaunchKernelGGL(k_msm_bucket_fold_wg<C>, dim3((unsigned)batch), dim3(FOLD_WG), 0, st, ws.rt, T1, xyzz_out,
+                         d_out, d_out_inf);
+      KZGX_TRY_HIP(hipGetLastError());
+      return KZGX_OK;
+    }
     // the fold's XYZZ results go to xyzz_out (chunked callers) or to the
     // start of bsum, which the fold no longer reads
     uint32_t* vx = xyzz_out ? xyzz_out : ws.bsum;

@@ -362,6 +362,99 @@ __global__ __launch_bounds__(64) void k_fixed_finish(const uint32_t* __restrict_
 }
 
 // --------------------------------------------------------------------------
+// latency path (a few MSMs of <= 2^14 points): every step below runs on
+// mostly idle CUs, so the time of one call is the longest dependent chain of
+// point additions, each ~5 us (mixed) / ~8 us (XYZZ) in one lane
+// (scripts/lat_micro.py).  The chain is cut to
+//   WG mixed additions (a thread owns one point and WG of its W windows)
+//   + 6 shuffle additions (wavefront fold inside the accumulation kernel)
+//   + Q / 64 - 1 + log2(min(Q, 64)) additions (one wavefront per MSM over the
+//     Q <= 256 wavefront partials, which then converts to affine in lane 0)
+// instead of W mixed additions + two 64:1 fold levels + a separate finish.
+// --------------------------------------------------------------------------
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_shfl_xor_add(const Xyzz<C>& acc, int off) {
+  constexpr int L = C::Fp29::L;
+  Xyzz<C> o;
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    o.X.v[k] = __shfl_xor(acc.X.v[k], off, 64);
+    o.Y.v[k] = __shfl_xor(acc.Y.v[k], off, 64);
+    o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], off, 64);
+    o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], off, 64);
+  }
+  return xyzz_add_impl<C>(acc, o);
+}
+
+// thread (g, i): point i < n_pad of MSM b, windows [g WG, min(W, (g + 1) WG));
+// wavefront partial q = (g n_pad + i) / 64 -> part[b][q]
+template <class C, int CB>
+__global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                        uint32_t n_pad, size_t stride_words,
+                                                        const uint32_t* __restrict__ tab, uint32_t n_t,
+                                                        const uint8_t* __restrict__ inf, int WG, uint32_t Q,
+                                                        uint32_t* __restrict__ part) {
+  constexpr int PW = packed_words<C>();
+  constexpr int XW = xyzz_words<C>();
+  constexpr int W = FixedWin<C, CB>::W;
+  constexpr uint32_t H = FixedWin<C, CB>::H;
+  const uint32_t b = blockIdx.y;
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;  // < G n_pad: grid is exact
+  const uint32_t g = t / n_pad, i = t - g * n_pad;
+  const int w0 = (int)g * WG, w1 = w0 + WG < W ? w0 + WG : W;
+  Xyzz<C> acc = xyzz_inf<C>();
+  if (i < n && !inf[i]) {
+    const uint32_t* sc = scalars + (size_t)b * stride_words + (size_t)i * 8;
+    uint32_t s[8];
+    {
+      const uint4 lo = reinterpret_cast<const uint4*>(sc)[0];
+      const uint4 hi = reinterpret_cast<const uint4*>(sc)[1];
+      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
+      s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+    }
+    scalar_reduce<C>(s);
+    const uint32_t* base = tab + (size_t)i * H * PW;
+    const size_t wstride = (size_t)n_t * H * PW;
+    uint32_t carry = 0;
+#pragma unroll 1
+    for (int w = 0; w < w1; w++) {
+      const int d = next_digit<CB>(s, carry);  // windows below w0 only carry
+      if (w < w0 || d == 0) continue;
+      Affine<C> cur =
+          packed_unpack<C>(packed_fetch<C>(base + (size_t)w * wstride + (size_t)((d < 0 ? -d : d) - 1) * PW));
+      if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
+      acc = xyzz_add_affine_impl<C>(acc, cur);
+    }
+  }
+#pragma unroll 1
+  for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
+  if (threadIdx.x == 0) xyzz_store<C>(part + ((size_t)b * Q + t / 64) * XW, acc);
+}
+
+// one wavefront per MSM: lane sums partials lane, lane + 64, ... < Q, a
+// shuffle tree over the lanes that hold any, lane 0 converts and stores
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_fold_finish(const uint32_t* __restrict__ part, uint32_t Q,
+                                                          uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  const uint32_t* p = part + (size_t)b * Q * XW;
+  Xyzz<C> acc = lane < Q ? xyzz_load<C>(p + (size_t)lane * XW) : xyzz_inf<C>();
+#pragma unroll 1
+  for (uint32_t k = lane + 64; k < Q; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(p + (size_t)k * XW));
+  int off = 32;
+  while (off > 1 && (uint32_t)off >= Q) off >>= 1;  // lanes >= Q hold the identity
+#pragma unroll 1
+  for (; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
+  if (lane == 0) {
+    Affine<C> a;
+    const bool fin = xyzz_to_affine<C>(acc, a);
+    affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+    out_inf[b] = fin ? 0u : 1u;
+  }
+}
+
+// --------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------
 constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
@@ -450,6 +543,27 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
                           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
   FixedTable& ft = ctx->fixed;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+  // latency path: a few MSMs of <= 2^14 points (k_fixed_accum_lat)
+  static const bool lat_off = std::getenv("KZGX_NO_FIXED_LAT") != nullptr;
+  const size_t n_pad = (n + 63) / 64 * 64;
+  if (batch <= 16 && !xyzz_out && n_pad <= 16384 && ft.pts_per_thread == 0 && !lat_off) {
+    constexpr int W = FixedWin<C, CB>::W;
+    // G window groups of WG windows: about 128 wavefront partials per MSM
+    int G = (int)std::min<size_t>(W, std::max<size_t>(1, 8192 / n_pad));
+    const int WG = (W + G - 1) / G;
+    G = (W + WG - 1) / WG;
+    const uint32_t Q = (uint32_t)(n_pad * G / 64);  // <= 256
+    MsmWs* wsp = ctx->ws_for(st);
+    if (!wsp) return KZGX_ERR_ARG;
+    KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
+    ProfScope p(ctx, st, "msm_accum");
+    hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
+                       (uint32_t)n_pad, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, WG, Q, wsp->fpart);
+    hipLaunchKernelGGL(k_fixed_fold_finish<C>, dim3((unsigned)batch), dim3(64), 0, st, wsp->fpart, Q, d_out,
+                       d_out_inf);
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
+  }
   // points per thread: 16 for batches (one MSM ~ 5 wavefronts at degree
   // 4096, T = 320 partials); for a few large MSMs, enough threads to fill
   // the 256 CUs x 4 SIMDs x 3 waves of resident slots
@@ -617,6 +731,82 @@ static int microbench_madd_impl(Ctx* ctx, double* rate) {
 int microbench_mixed_add(Ctx* ctx, double* rate) {
   return ctx->curve == KZGX_CURVE_BN254 ? microbench_madd_impl<BN254G1>(ctx, rate)
                                         : microbench_madd_impl<BLS12381G1>(ctx, rate);
+}
+
+// --------------------------------------------------------------------------
+// single-lane latency of the primitives on the latency-bound tails (the
+// finish kernels and the last reduction levels of one MSM): a dependent chain
+// of ITER operations in one lane of one wavefront, timed with the shader's
+// constant-rate wall clock and its core-clock counter inside the kernel
+// (no launch overhead).  op: 0 Montgomery product, 1 Fermat inversion,
+// 2 binary-Euclid inversion, 3 XYZZ addition, 4 mixed addition, 5 XYZZ ->
+// affine conversion.
+// --------------------------------------------------------------------------
+template <class C>
+__global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict__ pts, int op, uint32_t iters,
+                                                      uint64_t* __restrict__ out) {
+  using F = typename C::Fp29;
+  constexpr int PW = affine_words<C>();
+  if (threadIdx.x != 0) return;
+  const Affine<C> p = affine_load<C>(pts), q = affine_load<C>(pts + PW);
+  F29<F> a = p.x;
+  Xyzz<C> acc = xyzz_from_affine<C>(p);
+  const Xyzz<C> qx = xyzz_add_affine_impl<C>(xyzz_from_affine<C>(q), q);  // 2q, Z != 1
+  const uint64_t w0 = wall_clock64(), c0 = clock64();
+#pragma unroll 1
+  for (uint32_t k = 0; k < iters; k++) {
+    if (op == 0) a = f29_mul<F>(a, p.y);
+    else if (op == 1) a = f29_inv<F, C::Fp::N>(a, C::Fp::PM2);
+    else if (op == 2) a = f29_inv_vt<F, C::Fp::N>(a, C::Fp::P);
+    else if (op == 3) acc = xyzz_add_impl<C>(acc, qx);
+    else if (op == 4) acc = xyzz_add_affine_impl<C>(acc, q);
+    else {
+      Affine<C> r;
+      (void)xyzz_to_affine_impl<C>(acc, r);
+      acc.X = r.y;  // next input depends on this output
+    }
+  }
+  const uint64_t w1 = wall_clock64(), c1 = clock64();
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) o ^= a.v[i] ^ acc.X.v[i] ^ acc.ZZ.v[i];
+  out[0] = w1 - w0;
+  out[1] = c1 - c0;
+  out[2] = o;
+}
+
+template <class C>
+static int debug_latency_impl(Ctx* ctx, int op, uint32_t iters, double* res) {
+  if (ctx->n_srs < 2) return KZGX_ERR_NO_SRS;
+  constexpr int PW = affine_words<C>();
+  hipStream_t st = ctx->stream;
+  uint32_t* d_pts = nullptr;
+  uint64_t* d_out = nullptr;
+  KZGX_TRY_HIP(hipMalloc((void**)&d_pts, 2 * PW * 4));
+  if (hipMalloc((void**)&d_out, 3 * 8) != hipSuccess) {
+    (void)hipFree(d_pts);
+    return KZGX_ERR_HIP;
+  }
+  (void)hipMemcpyAsync(d_pts, ctx->d_table, 2 * PW * 4, hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(k_debug_latency<C>, dim3(1), dim3(64), 0, st, d_pts, op, 1u, d_out);  // warm
+  hipLaunchKernelGGL(k_debug_latency<C>, dim3(1), dim3(64), 0, st, d_pts, op, iters, d_out);
+  uint64_t h[3] = {0, 0, 0};
+  hipError_t e = hipMemcpyAsync(h, d_out, sizeof h, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d_pts);
+  (void)hipFree(d_out);
+  KZGX_TRY_HIP(e);
+  int khz = 0;
+  KZGX_TRY_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+  res[0] = (double)h[0] / iters / (khz * 1e3) * 1e9;  // ns per operation
+  res[1] = (double)h[1] / iters;                      // core clocks per operation
+  return KZGX_OK;
+}
+
+int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res) {
+  if (op < 0 || op > 5 || iters == 0) return KZGX_ERR_ARG;
+  return ctx->curve == KZGX_CURVE_BN254 ? debug_latency_impl<BN254G1>(ctx, op, iters, res)
+                                        : debug_latency_impl<BLS12381G1>(ctx, op, iters, res);
 }
 
 }  // namespace kzgx

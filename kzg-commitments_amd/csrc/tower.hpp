@@ -160,7 +160,7 @@ template <class C>
 KZGX_TW Fp2<C> f2_inv(const Fp2<C>& x) {
   using F = typename C::Fp29;
   const F29<F> t = fp_add<F>(f29_sqr<F>(x.a), f29_sqr<F>(x.b));
-  const F29<F> ti = f29_inv<F, C::Fp::N>(t, C::Fp::PM2);
+  const F29<F> ti = f29_inv_fast<F, C::Fp::N>(t, C::Fp::P, C::Fp::PM2);
   return Fp2<C>{f29_mul<F>(x.a, ti), fp_neg<F>(f29_mul<F>(x.b, ti))};
 }
 template <class C>

@@ -18,7 +18,7 @@ ctx = kzgx.Context("BN254")
 ctx.gen_srs(K.default_tau(C), 5000)
 P = np.array([[(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)] for v in K.random_scalars(C, 4097, 5)],
              dtype=np.uint64)
-for tag in ("pippenger", "table"):
+for tag in os.environ.get("LAT_TAGS", "pippenger,table").split(","):
     if tag == "table":
         ctx.set_fixed_base(16, 4097)
         ctx.set_fixed_points_per_thread(0)
