@@ -859,8 +859,14 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
     hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
                        ws.bsum, ws.rt);
-    static const bool fold_wave = std::getenv("KZGX_PIP_WAVE_FOLD") != nullptr;  // A/B: the one-wavefront fold
-    if (T1 % FOLD_WG == 0 && !fold_wave) {
+    // workgroup fold (affine conversion inline) for small batches, where four
+    // wavefronts per MSM are what fills the chip; from 256 MSMs the
+    // one-wavefront fold + thread-per-MSM finish is faster (measured, BN254
+    // c = 12: B = 128 wg +2.4%; B = 512 wave +2.8%; B = 2048 wave +6.7%,
+    // profiles/r02_s3_pip_fold_ab.json).  KZGX_PIP_WAVE_FOLD forces the
+    // wavefront form at every batch size (A/B).
+    static const bool fold_wave = std::getenv("KZGX_PIP_WAVE_FOLD") != nullptr;
+    if (T1 % FOLD_WG == 0 && batch < 256 && !fold_wave) {
       hipLaunchKernelGGL(k_msm_bucket_fold_wg<C>, dim3((unsigned)batch), dim3(FOLD_WG), 0, st, ws.rt, T1, xyzz_out,
                          d_out, d_out_inf);
       KZGX_TRY_HIP(hipGetLastError());

@@ -66,6 +66,27 @@ def test_msm_batch_identity(name, C, ctx_factory):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("batch", [255, 256])
+def test_msm_batch_fold_forms(name, C, batch, ctx_factory):
+    """Pippenger's bucket fold switches form at 256 MSMs per call (workgroup
+    fold with inline affine conversion below, wavefront fold + finish kernel
+    from there): both sides of the switch, every MSM checked"""
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    n = 65
+    ctx.gen_srs(tau, n)
+    rng = np.random.default_rng(0xF01D + batch)
+    S = rng.integers(0, 2**63, size=(batch, n, 4), dtype=np.uint64)
+    S[..., 3] &= np.uint64((1 << 59) - 1)  # < 2^251 < r: canonical
+    S[7] = 0                               # zero polynomial -> infinity
+    S[9, 1:] = 0                           # constant polynomial
+    out, inf = ctx.msm_batch(S.reshape(batch * n, 4), n, batch)
+    for b in range(batch):
+        coeffs = [sum(int(S[b, i, k]) << (64 * k) for k in range(4)) for i in range(n)]
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, coeffs), b
+
+
+@pytest.mark.parametrize("name,C", CURVES)
 @pytest.mark.parametrize("tau", [0, 1, 2, -1])
 def test_degenerate_srs(name, C, tau, ctx_factory, oracle_c):
     """tau = 0 gives infinite SRS points, tau = +-1 repeats points (bucket doublings)."""
