@@ -594,6 +594,40 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         for c in reversed([to_int(r) for r in coeffs_h]):
             ptau = (ptau * tau + c) % C.r
         ok = got == K.scalar_mul(C, (C.gx, C.gy), ptau)
+        ms_per_step = elapsed / args.steps * 1e3
+        # algorithmic bytes of one commit: n (affine point + 32 B scalar) + affine out
+        P_b = 2 * w64 * 8
+        unit_bytes = n * (P_b + 32) + P_b
+        achieved = unit_bytes / (ms_per_step * 1e-3) / 1e9
+        wins = ((C.r.bit_length() + 1 + fixed_bits - 1) // fixed_bits) if fixed_bits else \
+            (257 + args.window_bits - 1) // args.window_bits
+        madd_rate = n * wins / (ms_per_step * 1e-3)  # all ranks' mixed additions per second
+        peak = None
+        try:
+            peak = ctx.microbench_mixed_add() * world  # measured on this rank's GPU, times the ranks
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the headline
+            print("bench: mixed-add microbenchmark unavailable: %s" % e, file=sys.stderr)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
+            # the naive CPU commit of 2^20 + 1 terms takes minutes, so
+            # time the first 2^14 terms and scale linearly (the algorithm is one
+            # independent scalar multiplication per term)
+            import corc
+            corc.build()
+            m = 1 << 14
+            srs = corc.gen_srs("BN254", tau, m)
+            tc0 = time.perf_counter()
+            corc.msm_naive("BN254", srs, coeffs_h[:m])
+            tcpu = time.perf_counter() - tc0
+            cpu = {
+                "value": 1.0 / (tcpu * n / m),
+                "unit": "commits/s",
+                "cores": 1,
+                "kind": "port",
+                "sample": "first %d of the %d terms of the same commit on the C restatement of polyeval_G1 "
+                          "(oracle/kzg_oracle.c: naive per-term double-and-add, no GLV), 1 thread, %.1f s, "
+                          "scaled linearly to the full commit" % (m, n, tcpu),
+            }
         line = {
             "metric": "KZG commits/sec, BN254 degree-2^20, sharded",
             "value": args.steps / elapsed,
@@ -613,8 +647,29 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                            fixed_bits, ctx.fixed_base_info()[2] / 1e9)) if fixed_bits else
                               ("pippenger, c=%d, segment %d" % (args.window_bits, args.segment)),
                        "parallelism": "msm-shard%d" % world},
-            "secondary": {"fixed_table_setup_s": t_setup},
+            "roofline": {
+                "kernel": "msm_accum (one MSM per rank) + all-gather + fold",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS * world,
+                "unit": "GB/s",
+                "frac": achieved / (HBM_PEAK_GBS * world),
+                "traffic": None,
+                "algorithmic_bytes_per_step": unit_bytes,
+                "achieved_from": "algorithmic bytes of one commit / ms_per_step",
+                "note": "integer-VALU bound (no MFMA); see secondary.valu_roofline",
+            },
+            "secondary": {
+                "fixed_table_setup_s": t_setup,
+                "valu_roofline": None if not peak else {
+                    "achieved_mixed_adds_per_s": madd_rate,
+                    "peak_mixed_adds_per_s": peak,
+                    "frac": madd_rate / peak,
+                    "peak_from": "kzgx_microbench_mixed_add on rank 0's GPU x ranks, measured live",
+                },
+            },
             "parity": {"checked": 1, "ok": int(ok), "method": "[P(tau)]G1 identity"},
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

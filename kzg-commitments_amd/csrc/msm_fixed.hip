@@ -455,6 +455,84 @@ __global__ __launch_bounds__(64) void k_fixed_fold_finish(const uint32_t* __rest
 }
 
 // --------------------------------------------------------------------------
+// few large MSMs (cfg5: one 2^20-point commit over a table shard).  The
+// point-strided k_fixed_accum gives each thread ceil(n / T) whole points, so
+// with 2^20 points over the 196 608 resident lanes some SIMDs carry 3 waves x
+// 6 points while the average is 5.3: the busiest SIMD is 12.5% over the mean
+// (measured: 83% of the mixed-add peak).  Here the n W digit terms are
+// flattened point-major (term e = i W + w) and thread t owns the Q
+// consecutive terms [t Q, t Q + Q): every thread does Q or fewer additions.
+// A thread that starts inside point i runs the digit recoding of i's lower
+// windows for their carry only.  The lookup of the next term is in flight
+// during the addition of the current one, and the wavefront folds its 64
+// partials with 6 shuffle additions before one lane stores (the first 64:1
+// level of the reduction, without a launch).
+// --------------------------------------------------------------------------
+template <class C, int CB>
+__global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat(
+    const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
+    uint32_t n_t, const uint8_t* __restrict__ inf, uint32_t Q, uint32_t T, uint32_t* __restrict__ part) {
+  constexpr int PW = packed_words<C>();
+  constexpr int XW = xyzz_words<C>();
+  constexpr int W = FixedWin<C, CB>::W;
+  constexpr uint32_t H = FixedWin<C, CB>::H;
+  const uint32_t b = blockIdx.y;
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;  // < T: the grid is exact
+  const uint32_t* sc = scalars + (size_t)b * stride_words;
+  const size_t wstride = (size_t)n_t * H * PW;  // words between windows
+  const size_t e_end = (size_t)n * W;
+  size_t e = (size_t)t * Q;
+  const size_t e1 = e + Q < e_end ? e + Q : e_end;
+  Xyzz<C> acc = xyzz_inf<C>();
+  if (e < e1) {
+    // generator state: point i, window w, the scalar's remaining bits
+    uint32_t i = (uint32_t)(e / W);
+    int w = (int)(e - (size_t)i * W);
+    uint32_t s[8], carry = 0;
+    bool skip = false;  // infinity SRS point: all its terms are the identity
+    auto load = [&](uint32_t ii) {
+      const uint4 lo = reinterpret_cast<const uint4*>(sc + (size_t)ii * 8)[0];
+      const uint4 hi = reinterpret_cast<const uint4*>(sc + (size_t)ii * 8)[1];
+      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
+      s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+      scalar_reduce<C>(s);
+      carry = 0;
+      skip = inf[ii] != 0;
+    };
+    load(i);
+#pragma unroll 1
+    for (int k = 0; k < w; k++) (void)next_digit<CB>(s, carry);  // carry of the lower windows
+    int d = next_digit<CB>(s, carry);
+    if (skip) d = 0;
+    PackedPt<C> nx = packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
+                                     (size_t)((d < 0 ? -d : d) - (d != 0)) * PW);
+#pragma unroll 1
+    for (; e < e1; e++) {
+      Affine<C> cur = packed_unpack<C>(nx);
+      int dn = 0;
+      if (e + 1 < e1) {
+        if (++w == W) {
+          w = 0;
+          load(++i);
+        }
+        dn = next_digit<CB>(s, carry);
+        if (skip) dn = 0;
+        nx = packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
+                             (size_t)((dn < 0 ? -dn : dn) - (dn != 0)) * PW);
+      }
+      if (d != 0) {
+        if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
+        acc = xyzz_add_affine_impl<C>(acc, cur);
+      }
+      d = dn;
+    }
+  }
+#pragma unroll 1
+  for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
+  if (threadIdx.x == 0) xyzz_store<C>(part + ((size_t)b * (T / 64) + t / 64) * XW, acc);
+}
+
+// --------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------
 constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
@@ -568,6 +646,39 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   // 4096, T = 320 partials); for a few large MSMs, enough threads to fill
   // the 256 CUs x 4 SIMDs x 3 waves of resident slots
   constexpr size_t kSlots = 256 * 4 * 3 * 64;
+  // few large MSMs (>= 32 terms per resident lane): flattened terms, balanced
+  // to one addition per thread (k_fixed_accum_flat), T a multiple of 64^2
+  static const bool flat_off = std::getenv("KZGX_NO_FIXED_FLAT") != nullptr;
+  {
+    constexpr int W = FixedWin<C, CB>::W;
+    const size_t terms = n * (size_t)W;
+    if (batch <= 16 && !xyzz_out && ft.pts_per_thread == 0 && !flat_off && terms * batch >= 32 * kSlots) {
+      const uint32_t T = (uint32_t)std::max<size_t>(4096, kSlots / batch / 4096 * 4096);
+      const uint32_t Q = (uint32_t)((terms + T - 1) / T);
+      MsmWs* wsp = ctx->ws_for(st);
+      if (!wsp) return KZGX_ERR_ARG;
+      MsmWs& ws = *wsp;
+      KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * (T / 64) * XB, &ws.fpart_b));
+      KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * (T / 4096) * XB, &ws.fsum_b));
+      {
+        ProfScope p(ctx, st, "msm_accum");
+        hipLaunchKernelGGL((k_fixed_accum_flat<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
+                           (uint32_t)n, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, Q, T, ws.fpart);
+      }
+      ProfScope p(ctx, st, "msm_reduce");
+      // T / 64 wavefront partials per MSM: one more 64:1 level, then one
+      // wavefront per MSM over the T / 4096 left, then a thread per MSM
+      const size_t g2 = batch * (T / 4096);
+      hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((g2 + 3) / 4)), dim3(256), 0, st, ws.fpart, 64u,
+                         (uint32_t)g2, ws.fsum);
+      hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, st, ws.fsum,
+                         T / 4096, (uint32_t)batch, ws.fpart);
+      hipLaunchKernelGGL(k_fixed_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, ws.fpart,
+                         (uint32_t)batch, d_out, d_out_inf, nullptr);
+      KZGX_TRY_HIP(hipGetLastError());
+      return KZGX_OK;
+    }
+  }
   uint32_t P0 = ft.pts_per_thread;
   if (P0 == 0) P0 = batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
   uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));

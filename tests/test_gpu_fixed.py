@@ -190,3 +190,33 @@ def test_fixed_large_single_msm(name, C, batch, fresh_ctx):
     for b in range(batch):
         exp = K.commit_via_tau(C, tau, polys[b])
         assert pt(name, out[b], inf[b]) == exp
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("tau_kind,batch", [("default", 1), ("default", 2), ("zero", 1)])
+def test_fixed_flat_terms(name, C, tau_kind, batch, fresh_ctx):
+    """few large MSMs with >= 32 digit terms per resident lane take the
+    flattened-term kernel (k_fixed_accum_flat): threads start inside a point
+    (carry-only recoding of its lower windows), every thread ends on a term
+    boundary, and tau = 0 makes every SRS point but the first infinity (all of
+    its terms skipped).  c = 4: 64 windows, 100 003 points -> 33 terms per
+    thread; scalars with digit edge cases sit on both sides of thread
+    boundaries."""
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C) if tau_kind == "default" else 0
+    n, c = 100003, 4
+    ctx.gen_srs(tau, n)
+    ctx.set_fixed_base(c, n)
+    assert ctx.fixed_base_info()[:2] == (c, n)
+    H = 1 << (c - 1)
+    polys = []
+    for b in range(batch):
+        P = K.random_scalars(C, n, seed=4400 + b)
+        for j, i in enumerate((0, 1, 2, 3, 4, 5, 6, 7, 50000, 99999, n - 1)):
+            P[i] = [2, 1, C.r - 1, sum(H << (c * w) for w in range(63)) % C.r, (1 << 253) - 1,
+                    sum((H + 1) << (c * w) for w in range(62)) % C.r, 0, 0, C.r - 1, 1, 3][j]
+        polys.append(P)
+    S = np.concatenate([limbs(P) for P in polys])
+    out, inf = ctx.msm_batch(S, n, batch)
+    for b in range(batch):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
