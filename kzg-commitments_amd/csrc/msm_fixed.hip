@@ -502,29 +502,45 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
     load(i);
 #pragma unroll 1
     for (int k = 0; k < w; k++) (void)next_digit<CB>(s, carry);  // carry of the lower windows
-    int d = next_digit<CB>(s, carry);
-    if (skip) d = 0;
-    PackedPt<C> nx = packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
-                                     (size_t)((d < 0 ? -d : d) - (d != 0)) * PW);
+    // the digit of the current term and its table entry's address
+    auto fetch = [&](int dd) {
+      return packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
+                             (size_t)((dd < 0 ? -dd : dd) - (dd != 0)) * PW);
+    };
+    auto advance = [&]() {
+      if (++w == W) {
+        w = 0;
+        load(++i);
+      }
+      const int dd = next_digit<CB>(s, carry);
+      return skip ? 0 : dd;
+    };
+    int d0 = next_digit<CB>(s, carry);
+    if (skip) d0 = 0;
+    PackedPt<C> p0 = fetch(d0);
+    // two lookups in flight: terms e + 1 and e + 2 load during the addition
+    // of term e (one wave in three is ready to issue while the other two wait
+    // on random table lines)
+    int d1 = 0;
+    PackedPt<C> p1 = p0;
+    if (e + 1 < e1) {
+      d1 = advance();
+      p1 = fetch(d1);
+    }
 #pragma unroll 1
     for (; e < e1; e++) {
-      Affine<C> cur = packed_unpack<C>(nx);
-      int dn = 0;
-      if (e + 1 < e1) {
-        if (++w == W) {
-          w = 0;
-          load(++i);
-        }
-        dn = next_digit<CB>(s, carry);
-        if (skip) dn = 0;
-        nx = packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
-                             (size_t)((dn < 0 ? -dn : dn) - (dn != 0)) * PW);
+      Affine<C> cur = packed_unpack<C>(p0);
+      const int d = d0;
+      d0 = d1;
+      p0 = p1;
+      if (e + 2 < e1) {
+        d1 = advance();
+        p1 = fetch(d1);
       }
       if (d != 0) {
         if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
         acc = xyzz_add_affine_impl<C>(acc, cur);
       }
-      d = dn;
     }
   }
 #pragma unroll 1
@@ -653,7 +669,9 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
     constexpr int W = FixedWin<C, CB>::W;
     const size_t terms = n * (size_t)W;
     if (batch <= 16 && !xyzz_out && ft.pts_per_thread == 0 && !flat_off && terms * batch >= 32 * kSlots) {
-      const uint32_t T = (uint32_t)std::max<size_t>(4096, kSlots / batch / 4096 * 4096);
+      // KZGX_FLAT_TMULT: threads per resident-lane slot (A/B)
+      static const size_t tmult = std::getenv("KZGX_FLAT_TMULT") ? std::strtoul(std::getenv("KZGX_FLAT_TMULT"), nullptr, 10) : 1;
+      const uint32_t T = (uint32_t)std::max<size_t>(4096, kSlots * (tmult ? tmult : 1) / batch / 4096 * 4096);
       const uint32_t Q = (uint32_t)((terms + T - 1) / T);
       MsmWs* wsp = ctx->ws_for(st);
       if (!wsp) return KZGX_ERR_ARG;
