@@ -537,7 +537,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, max(count, 1), start)
     # fixed-base table over this rank's shard: the widest window whose table
-    # fits the budget (2^20 points on 1 GPU: c = 7, 198.6 GB; 2^17 per GPU on
+    # fits the budget (2^20 points on 1 GPU: c = 7, 158.9 GB; 2^17 per GPU on
     # 8 GPUs: c = 10, 139.6 GB).  Setup work, outside the timed region.
     t_setup = time.perf_counter()
     fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
