@@ -662,13 +662,13 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   // 4096, T = 320 partials); for a few large MSMs, enough threads to fill
   // the 256 CUs x 4 SIMDs x 3 waves of resident slots
   constexpr size_t kSlots = 256 * 4 * 3 * 64;
-  // few large MSMs (>= 32 terms per resident lane): flattened terms, balanced
+  // few large MSMs (>= 8 terms per resident lane): flattened terms, balanced
   // to one addition per thread (k_fixed_accum_flat), T a multiple of 64^2
   static const bool flat_off = std::getenv("KZGX_NO_FIXED_FLAT") != nullptr;
   {
     constexpr int W = FixedWin<C, CB>::W;
     const size_t terms = n * (size_t)W;
-    if (batch <= 16 && !xyzz_out && ft.pts_per_thread == 0 && !flat_off && terms * batch >= 32 * kSlots) {
+    if (batch <= 16 && !xyzz_out && ft.pts_per_thread == 0 && !flat_off && terms * batch >= 8 * kSlots) {
       // KZGX_FLAT_TMULT: threads per resident-lane slot (A/B)
       static const size_t tmult = std::getenv("KZGX_FLAT_TMULT") ? std::strtoul(std::getenv("KZGX_FLAT_TMULT"), nullptr, 10) : 1;
       const uint32_t T = (uint32_t)std::max<size_t>(4096, kSlots * (tmult ? tmult : 1) / batch / 4096 * 4096);
