@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0,
                     help="polynomials (cfg2/cfg4) or openings (cfg3) per GPU per step; default cfg2 2048, "
-                         "cfg4 1024, cfg3 4096 (BASELINE configs[2]: 4096 openings)")
+                         "cfg4 2048, cfg3 4096 (BASELINE configs[2]: 4096 openings)")
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "common"],
                     help="cfg2..cfg5: BASELINE.json configs[1..4]; common: benchmark.cpp --benchmark-common")
     ap.add_argument("--window-bits", type=int, default=12, help="signed-digit window (10..13)")
@@ -55,7 +55,8 @@ def parse():
                          "a window that does not fit steps down)")
     ap.add_argument("--fixed-ppt", type=int, default=-1,
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic; default cfg2 22: "
-                         "2048 MSMs x 3 wavefronts = two full residencies per launch, else 16)")
+                         "2048 MSMs x 3 wavefronts = two full residencies per launch; cfg4 65: 2048 x 1 wavefront; "
+                         "else 16)")
     ap.add_argument("--table-gb", type=float, default=200.0, help="cfg5: fixed-base table budget per GPU (GB)")
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
@@ -245,9 +246,14 @@ def main():
     # cfg2: 2048 polynomials x 22 points per thread (3 wavefronts per MSM, two
     # full residencies of the chip per launch): +2.9% over 1024 x 16 on one
     # box, interleaved (profiles/r02_ab_table_layout.json)
-    B = args.batch or {"cfg3": 4096, "cfg2": 2048}.get(args.workload, 1024)
+    # batch x points-per-thread shapes that fill whole residencies of the
+    # accumulation kernel's wavefront slots (BN254: 3 per SIMD = 3072; BLS12-381:
+    # 2 per SIMD = 2048): cfg2 2048 MSMs x 3 wavefronts (22 points per thread);
+    # cfg4 2048 x 1 (65 points per thread), measured +5% over 1024 x 16
+    # (profiles/r02_s3_cfg4_shape_ab.json)
+    B = args.batch or {"cfg3": 4096, "cfg2": 2048, "cfg4": 2048}.get(args.workload, 1024)
     if args.fixed_ppt < 0:
-        args.fixed_ppt = 22 if args.workload == "cfg2" else 16
+        args.fixed_ppt = {"cfg2": 22, "cfg4": 65}.get(args.workload, 16)
     ctx = kzgx.Context(curve, device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
