@@ -665,7 +665,11 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   // few large MSMs (>= 8 terms per resident lane): flattened terms, balanced
   // to one addition per thread (k_fixed_accum_flat), T a multiple of 64^2
   static const bool flat_off = std::getenv("KZGX_NO_FIXED_FLAT") != nullptr;
-  {
+  // instantiated for c <= 12 only: from c = 13 a table with 8 x 196 608 terms
+  // (BN254: >= 78 644 points x 20 windows x 4096 entries x 64 B = 422 GB) does
+  // not fit in HBM, so the path could never run (and each instantiation costs
+  // compile time)
+  if constexpr (CB <= 12) {
     constexpr int W = FixedWin<C, CB>::W;
     const size_t terms = n * (size_t)W;
     if (batch <= 16 && !xyzz_out && ft.pts_per_thread == 0 && !flat_off && terms * batch >= 8 * kSlots) {
