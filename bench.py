@@ -33,6 +33,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kzg-commitments_amd", "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# The exact launch shape of each throughput line: curve, MSMs per launch,
+# fixed-base window, SRS points per accumulation thread, streams per step.
+# tests/test_gpu_configs.py runs these shapes through make_step() and checks
+# every output; tests/test_bench_shapes.py pins them, so a changed default
+# fails a test until the test is changed with it.
+#   cfg2: 2048 MSMs x 3 wavefronts (22 points per thread): two full
+#         residencies of the chip's 3072 accumulation slots per launch
+#         (+2.9% over 1024 x 16, profiles/r02_ab_table_layout.json); c = 17
+#         (15 windows for 254-bit scalars, 257.8 GB)
+#   cfg3: one polynomial opened at x = 0..4095, one launch per step; 16
+#         points per thread beats 22 there (profiles/r02_s3_cfg4_shape_ab.json)
+#   cfg4: BLS12-381, 2048 x 1 wavefront (65 points per thread) = one
+#         residency at 2 waves per SIMD (+5% over 1024 x 16); c = 16 (255-bit
+#         scalars need 16 windows at c = 16 or 17)
+WORKLOAD_SHAPES = {
+    "cfg2": {"curve": "BN254", "batch": 2048, "fixed_bits": 17, "points_per_thread": 22, "streams": 2},
+    "cfg3": {"curve": "BN254", "batch": 4096, "fixed_bits": 17, "points_per_thread": 16, "streams": 1},
+    "cfg4": {"curve": "BLS12381", "batch": 2048, "fixed_bits": 16, "points_per_thread": 65, "streams": 2},
+}
+DEGREE = 4096      # BASELINE configs[1..3] (benchmark/benchmark.cpp:111)
+SRS_POINTS = 5000  # the reference benchmark's setup size
 REF_COMMIT_S = 1.104637  # README.md:132, BN254 degree 4096, 1 thread, unstated CPU
 REF_PROOF_S = 1.080747
 
@@ -69,6 +91,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pippenger", action="store_true",
                     help="skip the secondary Pippenger (table-less, create_commit's default) leg")
+    ap.add_argument("--no-table-curve", action="store_true",
+                    help="skip the throughput-vs-table-size leg (c = 10 .. 16 before the headline table)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-call latency leg (benchmark/benchmark.cpp's timed regions)")
     return ap.parse_args()
@@ -135,6 +159,112 @@ def set_fixed_with_fallback(kzgx, ctx, c, npts, budget=None):
 
 def to_int(row):
     return sum(int(row[i]) << (64 * i) for i in range(len(row)))
+
+
+def bench_inputs(C, workload, B, n, rank=0):
+    """seeded host inputs of one step: coefficients (1 or B polynomials of n
+    Fr limbs) and the opening points z"""
+    rng = np.random.default_rng(0x4B5A47 + rank)
+    zs_h = np.zeros((B, 4), dtype=np.uint64)
+    if workload == "cfg3":
+        # one degree-4096 polynomial opened at x = 0..B-1 (the reference's
+        # multi-proof benchmark's 4096 openings as single-opening proofs,
+        # SURVEY 8(a) a8)
+        coeffs_h = random_fr(rng, (1, n), C.r)
+        zs_h[:, 0] = np.arange(B, dtype=np.uint64)
+    else:
+        coeffs_h = random_fr(rng, (B, n), C.r)
+        zs_h[:, 0] = np.arange(B, dtype=np.uint64) % n
+    return coeffs_h, zs_h
+
+
+class StepBuffers:
+    """device inputs and outputs of one bench step"""
+
+    def __init__(self, torch, dev, coeffs_h, zs_h, w64):
+        B = zs_h.shape[0]
+        self.d_coeffs = torch.from_numpy(coeffs_h.view(np.int64)).to(dev)
+        self.d_z = torch.from_numpy(zs_h.view(np.int64)).to(dev)
+        self.d_cout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
+        self.d_cinf = torch.zeros((B,), dtype=torch.int32, device=dev)
+        self.d_pout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
+        self.d_pinf = torch.zeros((B,), dtype=torch.int32, device=dev)
+        self.d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
+
+
+def make_step(ctx, workload, n, bufs, streams, split=1, commit_first=False):
+    """one step: B commits (create_commit, n-point MSM) on streams[2s] and B
+    single-opening proofs (create_proof(poly, z, 1): quotient + (n-1)-point
+    MSM) on streams[2s + 1], cut into `split` sub-batches; cfg3 has no
+    commits and one shared polynomial"""
+    B = bufs.d_z.shape[0]
+    S = max(1, split)
+    cstride = 0 if workload == "cfg3" else n
+    cut = [B * s // S for s in range(S + 1)]
+
+    def step():
+        for s in range(S):
+            lo, hi = cut[s], cut[s + 1]
+            if hi == lo:
+                continue
+
+            def commits():
+                if workload != "cfg3":
+                    ctx.msm_batch_device(bufs.d_coeffs[lo].data_ptr(), n, hi - lo, n, bufs.d_cout[lo].data_ptr(),
+                                         bufs.d_cinf[lo:].data_ptr(), streams[2 * s].cuda_stream)
+
+            def proofs():
+                ctx.prove_single_batch_device(bufs.d_coeffs[0 if cstride == 0 else lo].data_ptr(), n, cstride,
+                                              bufs.d_z[lo].data_ptr(), hi - lo, bufs.d_pout[lo].data_ptr(),
+                                              bufs.d_pinf[lo:].data_ptr(), bufs.d_y[lo].data_ptr(),
+                                              streams[2 * s + 1].cuda_stream)
+
+            for f in ((commits, proofs) if commit_first else (proofs, commits)):
+                f()
+
+    return step
+
+
+def check_step(curve, C, tau, workload, coeffs_h, zs_h, bufs, w64):
+    """every output of the last step against the MSM-independent identity
+    (test infrastructure, outside the timed region): commit = [P(tau)]G1,
+    proof = [(P(tau) - P(z)) / (tau - z)]G1, y = P(z), with the C oracle's
+    Horner evaluation and scalar multiplication.  Returns (checked, ok,
+    first failure)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))  # checker only
+    import corc
+    corc.build()
+    cout = bufs.d_cout.cpu().numpy().view(np.uint64)
+    cinf = bufs.d_cinf.cpu().numpy()
+    pout = bufs.d_pout.cpu().numpy().view(np.uint64)
+    pinf = bufs.d_pinf.cpu().numpy()
+    ys = corc.limbs_to_ints(bufs.d_y.cpu().numpy().view(np.uint64))
+    G = (C.gx, C.gy)
+    B = zs_h.shape[0]
+    checked = ok = 0
+    bad = None
+    ptau_shared = corc.poly_eval(curve, coeffs_h[0], tau) if workload == "cfg3" else None
+
+    def got(row, inf):
+        return None if inf else (to_int(row[:w64]), to_int(row[w64:2 * w64]))
+
+    for b in range(B):
+        P = coeffs_h[0 if workload == "cfg3" else b]
+        ptau = ptau_shared if workload == "cfg3" else corc.poly_eval(curve, P, tau)
+        if workload != "cfg3":
+            checked += 1
+            good = got(cout[b], cinf[b]) == corc.scalar_mul(curve, G, ptau)
+            ok += good
+            bad = bad or (None if good else ("commit", b))
+        z = to_int(zs_h[b])
+        pz = corc.poly_eval(curve, P, z)
+        qt = (ptau - pz) * pow((tau - z) % C.r, -1, C.r) % C.r
+        checked += 2
+        g1 = got(pout[b], pinf[b]) == corc.scalar_mul(curve, G, qt)
+        g2 = ys[b] == pz
+        ok += int(g1) + int(g2)
+        bad = bad or (None if g1 else ("proof", b)) or (None if g2 else ("y", b))
+    return checked, ok, bad
 
 
 KERNELS = ("msm_count", "msm_scan", "msm_scatter", "msm_accum", "msm_reduce", "quotient_single")
@@ -204,14 +334,73 @@ def latency_leg(ctx, coeffs_h, reps=7):
         xs[:, 0] = np.arange(N, dtype=np.uint64)
         multi[str(N)] = median_ms(lambda: ctx.prove_range(P[:4096], xs), 3)
     out["multi_proof_ms"] = multi
+    # benchmark/benchmark.cpp:113-115: single commit / proof for degree
+    # 128 .. 4096 (README.md:127-132 publishes 30.1 / 42.5 ms at 128)
+    sweep = {}
+    for deg in (128, 256, 512, 1024, 2048, 4096):
+        Pd = P[:deg + 1]
+        sweep[str(deg)] = {"commit_ms": median_ms(lambda: ctx.msm(Pd), reps),
+                           "proof_ms": median_ms(lambda: ctx.prove_single_batch(Pd, z0), reps)}
+    out["degree_sweep"] = sweep
     return out
+
+
+def mads_per_mixed_add(L):
+    """v_mad_u64_u32 per XYZZ mixed addition (curve.hpp xyzz_add_affine_*):
+    6 products (L^2 + L^2 reduction), 2 squares (L(L+1)/2 + L^2) and one
+    two-product sum with one reduction (3 L^2) -- 1467 for BN254 (L = 9),
+    3542 for BLS12-381 (L = 14); the gfx950 ISA of k_fixed_accum holds exactly
+    these (scripts/isa_count.py, profiles/r03_isa_counts.json)"""
+    return 6 * 2 * L * L + 2 * (L * (L + 1) // 2 + L * L) + 3 * L * L
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_cmd(n, argv, port):
+    """the child command that runs `bench.py <argv>` as n ranks, one process
+    per GPU (the same form the driver uses for its multi-GPU runs)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` with no launcher around it: start the N ranks as a
+    child torch.distributed.run and wait.  This process never touches the GPU
+    (no torch import, no HIP call), so nothing is exec'ed from a process that
+    initialised the device.  Rank 0's JSON line reaches stdout through the
+    inherited descriptor; the exit status is the launcher's (non-zero when
+    any rank fails)."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(rank_launch_cmd(n, argv, free_port()), env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    if os.environ.get("KZGX_BENCH_LAUNCH_SELFTEST") == "1":
+        # launcher self-test (tests/test_bench_launcher.py, CPU only): report
+        # the rank layout and stop before anything touches a device
+        fail = os.environ.get("KZGX_BENCH_FAIL_RANK")
+        if fail is not None and int(fail) == rank:
+            return 3
+        if rank == 0:
+            print(json.dumps({"selftest": True, "world": world, "rank": rank, "gpus": args.gpus}), flush=True)
+        return 0
     import torch
     import torch.distributed as dist
 
@@ -238,46 +427,23 @@ def main():
     if args.workload == "common":
         return run_common(args, world, rank, local, dev, torch, dist, kzgx)
 
-    curve = "BLS12381" if args.workload == "cfg4" else "BN254"
+    shape = WORKLOAD_SHAPES[args.workload]
+    curve = shape["curve"]
     K, C = curve_consts(curve)
     tau = K.default_tau(C)
-    degree = 4096
+    degree = DEGREE
     n = degree + 1
-    # cfg2: 2048 polynomials x 22 points per thread (3 wavefronts per MSM, two
-    # full residencies of the chip per launch): +2.9% over 1024 x 16 on one
-    # box, interleaved (profiles/r02_ab_table_layout.json)
-    # batch x points-per-thread shapes that fill whole residencies of the
-    # accumulation kernel's wavefront slots (BN254: 3 per SIMD = 3072; BLS12-381:
-    # 2 per SIMD = 2048): cfg2 2048 MSMs x 3 wavefronts (22 points per thread);
-    # cfg4 2048 x 1 (65 points per thread), measured +5% over 1024 x 16
-    # (profiles/r02_s3_cfg4_shape_ab.json)
-    B = args.batch or {"cfg3": 4096, "cfg2": 2048, "cfg4": 2048}.get(args.workload, 1024)
+    B = args.batch or shape["batch"]
     if args.fixed_ppt < 0:
-        args.fixed_ppt = {"cfg2": 22, "cfg4": 65}.get(args.workload, 16)
+        args.fixed_ppt = shape["points_per_thread"]
     ctx = kzgx.Context(curve, device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
-    ctx.gen_srs(tau, 5000)
+    ctx.gen_srs(tau, SRS_POINTS)
     w64 = ctx.w64
 
-    rng = np.random.default_rng(0x4B5A47 + rank)
-    if args.workload == "cfg3":
-        # one degree-4096 polynomial opened at x = 0..B-1 (reference multi-proof
-        # benchmark's 4096 openings, as single-opening proofs)
-        coeffs_h = random_fr(rng, (1, n), C.r)
-        zs_h = np.zeros((B, 4), dtype=np.uint64)
-        zs_h[:, 0] = np.arange(B, dtype=np.uint64)
-    else:
-        coeffs_h = random_fr(rng, (B, n), C.r)
-        zs_h = np.zeros((B, 4), dtype=np.uint64)
-        zs_h[:, 0] = np.arange(B, dtype=np.uint64) % n
-    d_coeffs = torch.from_numpy(coeffs_h.view(np.int64)).to(dev)
-    d_z = torch.from_numpy(zs_h.view(np.int64)).to(dev)
-    d_cout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
-    d_cinf = torch.zeros((B,), dtype=torch.int32, device=dev)
-    d_pout = torch.zeros((B, 2 * w64), dtype=torch.int64, device=dev)
-    d_pinf = torch.zeros((B,), dtype=torch.int32, device=dev)
-    d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
+    coeffs_h, zs_h = bench_inputs(C, args.workload, B, n, rank)
+    bufs = StepBuffers(torch, dev, coeffs_h, zs_h, w64)
     # the commits and proofs of a step are independent batches: each runs on
     # its own stream (optionally cut into `split` sub-batches) so the short
     # latency-bound phases of one (reduction, affine conversion, quotient)
@@ -286,34 +452,13 @@ def main():
     streams = [torch.cuda.Stream(device=dev) for _ in range(2 * S)]
     if args.serial:
         streams = [streams[0]] * (2 * S)
-    cstride = 0 if args.workload == "cfg3" else n
-    cut = [B * s // S for s in range(S + 1)]
-
-    def step():
-        for s in range(S):
-            lo, hi = cut[s], cut[s + 1]
-            if hi == lo:
-                continue
-
-            def commits():
-                if args.workload != "cfg3":
-                    ctx.msm_batch_device(d_coeffs[lo].data_ptr(), n, hi - lo, n, d_cout[lo].data_ptr(),
-                                         d_cinf[lo:].data_ptr(), streams[2 * s].cuda_stream)
-
-            def proofs():
-                ctx.prove_single_batch_device(d_coeffs[0 if cstride == 0 else lo].data_ptr(), n, cstride,
-                                              d_z[lo].data_ptr(), hi - lo, d_pout[lo].data_ptr(),
-                                              d_pinf[lo:].data_ptr(), d_y[lo].data_ptr(),
-                                              streams[2 * s + 1].cuda_stream)
-
-            for f in ((commits, proofs) if args.commit_first else (proofs, commits)):
-                f()
+    step = make_step(ctx, args.workload, n, bufs, streams, S, args.commit_first)
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
     # c = 17 cuts BN254's 254-bit scalars to 15 windows (16 at c = 16: +7.8%
     # measured on one box, profiles/r02_ab_table_layout.json); BLS12-381's
     # 255-bit scalars need 16 windows at either width
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (17 if curve == "BN254" else 16)
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else shape["fixed_bits"]
 
     # ---- secondary legs on the default product path (no table): what
     # kzg::trusted_setup::create_commit / create_proof do without precompute()
@@ -327,6 +472,26 @@ def main():
     lat = None
     if not args.no_latency and args.workload != "cfg3":
         lat = {"pippenger": latency_leg(ctx, coeffs_h)}
+
+    # throughput vs table size: what a re-linked create_commit gets at each
+    # HBM budget (trusted_setup::precompute_budget picks the widest window
+    # that fits); c = 0 is Pippenger, the table-less default
+    curve_pts = None
+    if fixed_bits and not args.no_table_curve:
+        curve_pts = [{"window_bits": 0, "gb": 0.0, "value": pip["value"] if pip else None}]
+        ctx.set_fixed_points_per_thread(args.fixed_ppt)
+        for cc in (10, 12, 14, 16):
+            if cc >= fixed_bits:
+                continue
+            tb = time.perf_counter()
+            built = set_fixed_with_fallback(kzgx, ctx, cc, n)
+            tb = time.perf_counter() - tb
+            if built != cc:
+                continue
+            ce, _ = timed_run(ctx, step, streams, 4, 1, world, dist, torch, dev)
+            curve_pts.append({"window_bits": cc, "gb": ctx.fixed_base_info()[2] / 1e9, "setup_s": tb,
+                              "value": units_per_step * 4 * world / ce})
+        ctx.set_fixed_base(0, 0)
 
     t_setup = time.perf_counter()
     if fixed_bits:
@@ -343,29 +508,11 @@ def main():
 
     elapsed, kern = timed_run(ctx, step, streams, args.steps, args.warmup, world, dist, torch, dev)
 
-    # ---- parity spot check (oracle identity, MSM-independent) ----
+    # ---- parity: every output of the last step (oracle identity, MSM-independent) ----
     checked = ok = 0
+    bad = None
     if rank == 0:
-        cout = d_cout.cpu().numpy().view(np.uint64)
-        cinf = d_cinf.cpu().numpy()
-        pout = d_pout.cpu().numpy().view(np.uint64)
-        pinf = d_pinf.cpu().numpy()
-        G = (C.gx, C.gy)
-        for b in (0, B - 1):
-            pb = 0 if args.workload == "cfg3" else b
-            P = [to_int(row) for row in coeffs_h[pb]]
-            ptau = K.poly_eval(C, P, tau)
-            if args.workload != "cfg3":
-                exp = K.scalar_mul(C, G, ptau)
-                got = None if cinf[b] else (to_int(cout[b, :w64]), to_int(cout[b, w64:]))
-                checked += 1
-                ok += exp == got
-            z = to_int(zs_h[b])
-            qt = (ptau - K.poly_eval(C, P, z)) * pow((tau - z) % C.r, -1, C.r) % C.r
-            exp = K.scalar_mul(C, G, qt)
-            got = None if pinf[b] else (to_int(pout[b, :w64]), to_int(pout[b, w64:]))
-            checked += 1
-            ok += exp == got
+        checked, ok, bad = check_step(curve, C, tau, args.workload, coeffs_h, zs_h, bufs, w64)
 
     # ---- CPU baseline (rank 0, N = 1 only) ----
     cpu = None
@@ -386,6 +533,16 @@ def main():
             corc.msm_naive(curve, srs[: max(len(q), 1)], corc.ints_to_limbs(q, 4))
             nunits += 1
         tcpu = time.perf_counter() - tc0
+        # BASELINE configs[0]: degree-128 commit + single-opening proof on the
+        # CPU path (benchmark.cpp:40-66 at degree 128; README.md:127 reports
+        # 30.1 ms commit / 42.5 ms proof for the reference)
+        P128 = coeffs_h[0][:129]
+        t128 = time.perf_counter()
+        corc.msm_naive(curve, srs[:129], P128)
+        t128c = time.perf_counter() - t128
+        q128 = corc.quotient(curve, corc.limbs_to_ints(P128), 0, 1)
+        corc.msm_naive(curve, srs[: max(len(q128), 1)], corc.ints_to_limbs(q128, 4))
+        t128p = time.perf_counter() - t128 - t128c
         cpu_model = platform.processor()
         try:
             with open("/proc/cpuinfo") as f:
@@ -400,6 +557,8 @@ def main():
             "unit": "commits+proofs/s" if args.workload != "cfg3" else "proofs/s",
             "cores": 1,
             "kind": "port",
+            "configs0_degree128": {"commit_ms": t128c * 1e3, "proof_ms": t128p * 1e3,
+                                   "reference_published_ms": {"commit": 30.1, "proof": 42.5}},
             "sample": "%d %s at degree %d on the C restatement of the reference path (oracle/kzg_oracle.c: "
                       "naive per-term polyeval_G1 with left-to-right double-and-add scalar multiplication in "
                       "Jacobian coordinates, no GLV; quotient by evaluate + interpolate + long division), "
@@ -450,10 +609,22 @@ def main():
         madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * wins
         madd_rate = madds / (ms_per_step * 1e-3)
         peak = None
+        mad_peak = None
         try:
             peak = ctx.microbench_mixed_add()
+            mad_peak = ctx.microbench_mad_u64()
         except Exception as e:  # noqa: BLE001 -- reported, never fatal for the headline
-            print("bench: mixed-add microbenchmark unavailable: %s" % e, file=sys.stderr)
+            print("bench: VALU microbenchmarks unavailable: %s" % e, file=sys.stderr)
+        if curve_pts is not None and fb[0]:
+            curve_pts.append({"window_bits": fb[0], "gb": fb[2] / 1e9, "setup_s": t_setup, "value": value})
+        L = 9 if curve == "BN254" else 14
+        mpa = mads_per_mixed_add(L)
+        isa = None
+        try:
+            with open(os.path.join(ROOT, "profiles", "r03_isa_counts.json")) as f:
+                isa = json.load(f).get("%s_c%d" % (curve, fb[0]))
+        except (OSError, ValueError):
+            isa = None
         line = {
             "metric": "KZG commits/sec + proofs/sec, %s degree-4096" % curve,
             "value": value,
@@ -510,14 +681,30 @@ def main():
                     "peak_from": "kzgx_microbench_mixed_add: the accumulation loop's XYZZ mixed add on "
                                  "register-resident operands at the kernel's occupancy, whole GPU, measured live",
                 },
+                "mad_issue": None if not mad_peak else {
+                    "mads_per_mixed_add": mpa,
+                    "achieved_mad_lane_ops_per_s": madd_rate * mpa,
+                    "peak_mad_lane_ops_per_s": mad_peak,
+                    "frac": madd_rate * mpa / mad_peak,
+                    "valu_per_mixed_add_isa": isa,
+                    "peak_from": "kzgx_microbench_mad_u64: v_mad_u64_u32 in asm, 8 independent chains per lane, "
+                                 "whole GPU, measured live (the hardware issue ceiling of the instruction every "
+                                 "partial product is)",
+                },
+                "table_curve": curve_pts,
                 "pippenger": pip,
                 "latency": lat,
             },
-            "parity": {"checked": checked, "ok": int(ok), "method": "[P(tau)]G1 / [q(tau)]G1 identity"},
+            "parity": {"checked": checked, "ok": int(ok), "first_failure": bad,
+                       "method": "every output of the last step: commit = [P(tau)]G1, proof = [q(tau)]G1, "
+                                 "y = P(z) (C oracle)"},
             "cpu_baseline": cpu,
             "reference_published": {"commit_ms": REF_COMMIT_S * 1e3, "proof_ms": REF_PROOF_S * 1e3,
                                     "multi_proof_ms": {"128": 922.247, "256": 860.305, "512": 810.811,
                                                        "1024": 800.158, "2048": 745.346},
+                                    "degree_sweep_ms": {"128": [30.083, 42.504], "256": [55.151, 62.676],
+                                                        "512": [136.220, 122.255], "1024": [211.453, 267.592],
+                                                        "2048": [445.452, 446.845], "4096": [1104.637, 1080.747]},
                                     "source": "README.md:127-139 (BN254, unstated CPU, 1 thread); "
                                               "throughput equivalent %.3f commits+proofs/s" % (
                                                   2.0 / (REF_COMMIT_S + REF_PROOF_S))},
@@ -759,4 +946,4 @@ def run_common(args, world, rank, local, dev, torch, dist, kzgx):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -187,10 +187,20 @@ class trusted_setup {
   std::vector<G2> g2_points() const;
   /** Extension: precompute the fixed-base table of signed-digit multiples
    *  for the first `points` SRS points (0 = all) with `window_bits`-bit
-   *  windows (kzgx_set_fixed_base; BN254 c = 16 over 4097 points takes
-   *  171.8 GB of HBM).  Commits and proofs over that prefix then run as plain
-   *  table sums.  window_bits = 0 drops the table. */
+   *  windows (kzgx_set_fixed_base).  Entries are 64 B (BN254) / 112 B
+   *  (BLS12-381); over 4097 points BN254 c = 17 (15 windows, the bench's
+   *  table) takes 257.8 GB of HBM, c = 16 137.5 GB, c = 12 11.8 GB, and
+   *  BLS12-381 c = 16 240.6 GB.  Commits and proofs over that prefix then run
+   *  as plain table sums.  window_bits = 0 drops the table.  The reference's
+   *  create_commit allocates nothing beyond the SRS
+   *  (src/trusted_setup.cpp:137-142): without a precompute call every MSM
+   *  runs on Pippenger. */
   void precompute(int window_bits = 16, size_t points = 0);
+  /** Extension: the widest window whose table over `points` SRS points
+   *  (0 = all) fits `budget_bytes` and the free HBM; returns the window
+   *  built (0: none fits, Pippenger stays).  DESIGN.md section 3 holds the
+   *  measured throughput at each table size. */
+  int precompute_budget(size_t budget_bytes, size_t points = 0);
 };
 
 }  // namespace kzg

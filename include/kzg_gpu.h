@@ -97,6 +97,15 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
 int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
 /* built table: window bits (0 = none), points covered, device bytes */
 int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
+/* device bytes a table of window c over n_points would take (no context) */
+int kzgx_fixed_base_bytes(int curve, int c, size_t n_points, size_t* bytes);
+/* bounded-memory precompute: the widest supported window c <= 17 whose
+ * table over n_points fits budget_bytes AND the device's free memory
+ * (less a 4 GiB margin for workspaces); builds it (as kzgx_set_fixed_base)
+ * and returns it in *c_out, or installs no table (*c_out = 0: every MSM on
+ * Pippenger) when even c = 7 does not fit.  Extension with no reference
+ * counterpart: trusted_setup::precompute_budget. */
+int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_points, int* c_out);
 /* SRS points summed per accumulation thread on the fixed-base path
  * (0 = automatic, the default: 16 for batches of >= 64 MSMs, else enough
  * threads to fill the GPU, with a wavefront-level fold for single MSMs) */
@@ -106,6 +115,10 @@ int kzgx_set_fixed_points_per_thread(kzgx_ctx* ctx, unsigned p);
  * L1-resident operands over the whole GPU -- the VALU ceiling the bench's
  * valu_roofline divides by.  Needs an SRS (its first points are the operands). */
 int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s);
+/* measurement: the hardware issue ceiling of v_mad_u64_u32 (lane
+ * operations per second; 8 independent chains per lane, whole GPU) -- the
+ * denominator of the bench's mad_issue roofline */
+int kzgx_microbench_mad_u64(kzgx_ctx* ctx, double* lane_ops_per_s);
 
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */

@@ -36,6 +36,15 @@
 #define KZGX_NEG_Y1(y) f29_sub<F>(f29_zero<F>(), (y), F::P4)
 #endif
 
+// scheduling fence between the product groups of the chained mixed addition
+// (keeps the scheduler from overlapping groups, which raises register
+// pressure past the accumulation kernels' budget)
+#ifdef KZGX_NO_GROUP_FENCE
+#define KZGX_GROUP_FENCE() ((void)0)
+#else
+#define KZGX_GROUP_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 namespace kzgx {
 
 template <class C>
@@ -132,9 +141,11 @@ KZGX_DEV Xyzz<C> xyzz_dbl_impl(const Xyzz<C>& p) {
   return r;
 }
 
-// p + a, a affine and finite (madd-2008-s)
+// p + a, a affine and finite (madd-2008-s), one product at a time (the
+// compiler splits each column into two mad chains and merges them: kept for
+// A/B against xyzz_add_affine_nway, scripts/micro_madd.hip)
 template <class C>
-KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
+KZGX_DEV Xyzz<C> xyzz_add_affine_classic(const Xyzz<C>& p, const Affine<C>& a) {
   using F = typename C::Fp29;
 #ifdef KZGX_LAZY_NEG_Y1
   if (xyzz_is_inf<C>(p)) {  // keep Y normalized (a.y may be a lazy negation)
@@ -166,6 +177,89 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
   r.ZZ = f29_mul<F>(p.ZZ, PP);
   r.ZZZ = f29_mul<F>(p.ZZZ, PPP);
   return r;
+}
+
+// p + a as xyzz_add_affine_classic (same formulas, same value bounds, the
+// same field values), with every product's columns as single mad chains
+// (field29.hpp, "chained forms": no per-column merge of two partial
+// chains).  KZGX_NWAY_PAIRS: independent products side by side --
+// (U2, S2), (PPP, Q), (ZZ3, ZZZ3) -- otherwise one product at a time.
+// The order keeps few values live: P^2 before (PPP, Q), R^2 after it, Y3
+// before ZZ3 / ZZZ3.
+#ifndef KZGX_NWAY_PAIRS
+#define KZGX_NWAY_PAIRS 1
+#endif
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
+  using F = typename C::Fp29;
+#ifdef KZGX_LAZY_NEG_Y1
+  if (xyzz_is_inf<C>(p)) {
+    Xyzz<C> r = xyzz_from_affine<C>(a);
+    r.Y = f29_normalize<F>(a.y);
+    return r;
+  }
+#else
+  if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
+#endif
+  F29<F> U2, S2;
+#if KZGX_NWAY_PAIRS
+  f29_mul_x2<F>(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
+#else
+  U2 = f29_mul_chain<F>(a.x, p.ZZ);
+  S2 = f29_mul_chain<F>(a.y, p.ZZZ);
+#endif
+  const F29<F> P = f29_sub<F>(U2, p.X, F::P8);          // < 10m
+  const F29<F> R = f29_sub<F>(S2, p.Y, F::P4);          // < 6m
+  const F29<F> PP = f29_sqr_chain<F>(P);                // < 2m
+  if (f29_is_zero_lt2m<F>(PP)) {  // x equal: double or cancel
+    if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);
+    return xyzz_inf<C>();
+  }
+  F29<F> PPP, Q;
+#if KZGX_NWAY_PAIRS
+  f29_mul_x2<F>(P, PP, p.X, PP, PPP, Q);
+#else
+  PPP = f29_mul_chain<F>(P, PP);
+  Q = f29_mul_chain<F>(p.X, PP);
+#endif
+  const F29<F> RR = f29_sqr_chain<F>(R);
+  Xyzz<C> r;
+  r.X = f29_sub<F>(RR, f29_add_2x_lazy<F>(PPP, Q), F::P6);  // < 8m
+  // Y3 = R (Q - X3) + (-Y1) PPP with one reduction
+  r.Y = f29_mul2_chain<F>(R, f29_sub<F>(Q, r.X, F::P8), KZGX_NEG_Y1(p.Y), PPP);
+#if KZGX_NWAY_PAIRS
+  f29_mul_x2<F>(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
+#else
+  r.ZZ = f29_mul_chain<F>(p.ZZ, PP);
+  r.ZZZ = f29_mul_chain<F>(p.ZZZ, PPP);
+#endif
+  return r;
+}
+
+// the mixed addition every accumulation loop inlines: 0 = classic (one
+// product at a time), 1 = grouped independent products (nway)
+#ifndef KZGX_MADD_VARIANT
+#define KZGX_MADD_VARIANT 1
+#endif
+template <class C, int V>
+KZGX_DEV Xyzz<C> xyzz_add_affine_v(const Xyzz<C>& p, const Affine<C>& a) {
+  if constexpr (V == 0) {
+    return xyzz_add_affine_classic<C>(p, a);
+  } else if constexpr (V == 1) {
+    return xyzz_add_affine_nway<C>(p, a);
+  } else {  // V == 2: no arithmetic, the operand only consumed (memory-path probe for scripts/micro_madd.hip)
+    Xyzz<C> r = p;
+#pragma unroll
+    for (int i = 0; i < C::Fp29::L; i++) {
+      r.X.v[i] ^= a.x.v[i];
+      r.Y.v[i] ^= a.y.v[i];
+    }
+    return r;
+  }
+}
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
+  return xyzz_add_affine_v<C, KZGX_MADD_VARIANT>(p, a);
 }
 
 // p + q (add-2008-s)

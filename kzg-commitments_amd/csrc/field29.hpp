@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "curve_consts.h"
 
 #ifndef KZGX_DEV
@@ -194,6 +196,215 @@ KZGX_DEV F29<F> f29_mul2(const F29<F>& a, const F29<F>& b, const F29<F>& c, cons
   }
   t.v[L - 1] = (uint32_t)acc;
   return t;
+}
+
+// acc += x y with the sum pinned to one dependent chain (the asm is an
+// opaque identity on acc: the compiler can neither re-associate the column
+// into two chains nor merge them back with a 64-bit add)
+KZGX_DEV void mad_chain(uint64_t& acc, uint32_t x, uint32_t y) {
+#if defined(KZGX_MAD_S100)
+  asm("v_mad_u64_u32 %0, s[100:101], %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "s100", "s101");
+#elif defined(KZGX_MAD_VCC)
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "vcc");
+#else
+  acc += (uint64_t)x * y;
+  asm("" : "+v"(acc));
+#endif
+}
+// the same with a wave-uniform second factor (a modulus limb in an SGPR)
+KZGX_DEV void mad_chain_s(uint64_t& acc, uint32_t x, uint32_t y_uniform) {
+#if defined(KZGX_MAD_S100)
+  asm("v_mad_u64_u32 %0, s[100:101], %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y_uniform) : "s100", "s101");
+#elif defined(KZGX_MAD_VCC)
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y_uniform) : "vcc");
+#else
+  acc += (uint64_t)x * y_uniform;
+  asm("" : "+v"(acc));
+#endif
+}
+
+// compile-time loop: f(std::integral_constant<int, K>) for K in [K0, K1)
+template <int K0, int K1, class Fn>
+KZGX_DEV void static_for(Fn&& f) {
+  if constexpr (K0 < K1) {
+    f(std::integral_constant<int, K0>{});
+    static_for<K0 + 1, K1>(f);
+  }
+}
+
+// One Montgomery product's column state for the chained forms below: the
+// 64-bit column accumulator and the reduction digits so far.
+template <class F>
+struct MontChain {
+  uint64_t acc;
+  uint32_t q[F::L];
+};
+
+// column K of a b into the chain
+template <class F, int K>
+KZGX_DEV void mc_prod(MontChain<F>& c, const F29<F>& a, const F29<F>& b) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int j = K - i;
+    if (j >= 0 && j < F::L) mad_chain(c.acc, a.v[i], b.v[j]);
+  }
+}
+
+// column K of a^2 (dd = 2a limb-wise)
+template <class F, int K>
+KZGX_DEV void mc_sqr(MontChain<F>& c, const F29<F>& a, const F29<F>& dd) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int j = K - i;
+    if (j > i && j < F::L) mad_chain(c.acc, a.v[i], dd.v[j]);
+  }
+  if constexpr ((K & 1) == 0 && (K >> 1) < F::L) mad_chain(c.acc, a.v[K >> 1], a.v[K >> 1]);
+}
+
+// the reduction terms of column K, then its digit (K < L) or output limb,
+// then the carry into column K + 1
+template <class F, int K>
+KZGX_DEV void mc_reduce(MontChain<F>& c, F29<F>& r, const uint32_t (&pl)[F::L]) {
+  constexpr int L = F::L;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    const int j = K - i;
+    if (i < K && j >= 1 && j < L) mad_chain_s(c.acc, c.q[i], pl[j]);
+  }
+  if constexpr (K < L) {
+    c.q[K] = ((uint32_t)c.acc * F::INV) & M29;
+    mad_chain_s(c.acc, c.q[K], pl[0]);
+  } else {
+    r.v[K - L] = (uint32_t)c.acc & M29;
+  }
+  c.acc >>= 29;
+  if constexpr (K == 2 * L - 2) r.v[L - 1] = (uint32_t)c.acc;
+}
+
+// the modulus limbs as the opaque uniform values of f29_pl, once per call
+template <class F>
+struct PLimbs {
+  uint32_t v[F::L];
+  KZGX_DEV PLimbs() {
+#pragma unroll
+    for (int j = 0; j < F::L; j++) {
+#ifdef KZGX_PL_SGPR
+      v[j] = f29_pl<F>(j);
+#else
+      asm("" : "=v"(v[j]) : "0"(F::P[j]));
+#endif
+    }
+  }
+};
+
+// Independent Montgomery products computed side by side, every column of
+// every product ONE dependent v_mad_u64_u32 chain that starts from the
+// previous column's carry: a shift per column and no merge of two partial
+// chains (the compiler splits a lone product's columns into two chains for
+// latency and pays a 64-bit add per column to join them).  The chains of the
+// different products are independent, so the scheduler interleaves them.
+// Same output bounds as f29_mul / f29_sqr / f29_mul2.
+template <class F>
+KZGX_DEV void f29_mul_x2(const F29<F>& a0, const F29<F>& b0, const F29<F>& a1, const F29<F>& b1, F29<F>& r0,
+                         F29<F>& r1) {
+  const PLimbs<F> pl;
+  MontChain<F> c0, c1;
+  c0.acc = c1.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_prod<F, k>(c0, a0, b0);
+    mc_prod<F, k>(c1, a1, b1);
+    mc_reduce<F, k>(c0, r0, pl.v);
+    mc_reduce<F, k>(c1, r1, pl.v);
+  });
+}
+
+template <class F>
+KZGX_DEV void f29_sqr_x2(const F29<F>& a0, const F29<F>& a1, F29<F>& r0, F29<F>& r1) {
+  F29<F> d0, d1;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    d0.v[i] = a0.v[i] << 1;
+    d1.v[i] = a1.v[i] << 1;
+  }
+  const PLimbs<F> pl;
+  MontChain<F> c0, c1;
+  c0.acc = c1.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_sqr<F, k>(c0, a0, d0);
+    mc_sqr<F, k>(c1, a1, d1);
+    mc_reduce<F, k>(c0, r0, pl.v);
+    mc_reduce<F, k>(c1, r1, pl.v);
+  });
+}
+
+// a b / R as f29_mul, each column one chain
+template <class F>
+KZGX_DEV F29<F> f29_mul_chain(const F29<F>& a, const F29<F>& b) {
+  const PLimbs<F> pl;
+  MontChain<F> h;
+  h.acc = 0;
+  F29<F> r;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_prod<F, k>(h, a, b);
+    mc_reduce<F, k>(h, r, pl.v);
+  });
+  return r;
+}
+
+// a^2 / R as f29_sqr, each column one chain
+template <class F>
+KZGX_DEV F29<F> f29_sqr_chain(const F29<F>& a) {
+  F29<F> dd;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) dd.v[i] = a.v[i] << 1;
+  const PLimbs<F> pl;
+  MontChain<F> h;
+  h.acc = 0;
+  F29<F> r;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_sqr<F, k>(h, a, dd);
+    mc_reduce<F, k>(h, r, pl.v);
+  });
+  return r;
+}
+
+// (a b + c d) / R as f29_mul2, each column one chain
+template <class F>
+KZGX_DEV F29<F> f29_mul2_chain(const F29<F>& a, const F29<F>& b, const F29<F>& c, const F29<F>& d) {
+  const PLimbs<F> pl;
+  MontChain<F> h;
+  h.acc = 0;
+  F29<F> r;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_prod<F, k>(h, a, b);
+    mc_prod<F, k>(h, c, d);
+    mc_reduce<F, k>(h, r, pl.v);
+  });
+  return r;
+}
+
+// r0 = (a0 b0 + c0 d0) / R (one reduction), r1 = a1 b1 / R, r2 = a2 b2 / R
+template <class F>
+KZGX_DEV void f29_mul2_x3(const F29<F>& a0, const F29<F>& b0, const F29<F>& c0, const F29<F>& d0, const F29<F>& a1,
+                          const F29<F>& b1, const F29<F>& a2, const F29<F>& b2, F29<F>& r0, F29<F>& r1, F29<F>& r2) {
+  const PLimbs<F> pl;
+  MontChain<F> h0, h1, h2;
+  h0.acc = h1.acc = h2.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_prod<F, k>(h0, a0, b0);
+    mc_prod<F, k>(h0, c0, d0);
+    mc_prod<F, k>(h1, a1, b1);
+    mc_prod<F, k>(h2, a2, b2);
+    mc_reduce<F, k>(h0, r0, pl.v);
+    mc_reduce<F, k>(h1, r1, pl.v);
+    mc_reduce<F, k>(h2, r2, pl.v);
+  });
 }
 
 // Montgomery square: cross products once, against a doubled operand

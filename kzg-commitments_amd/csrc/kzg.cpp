@@ -7,6 +7,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <map>
 #include <mutex>
 #include <random>
 
@@ -19,9 +20,13 @@ int CURVE_ORDER_BYTES;
 namespace {
 
 int g_curve = KZGX_CURVE_BN254;
-kzgx_ctx* g_ctx = nullptr;  // default context for setup-independent poly ops
-int g_device = 0;          // kzg::set_device
+int g_device = 0;  // kzg::set_device
 std::mutex g_mu;
+// default contexts for the setup-independent poly ops, one per (curve,
+// device), created on first use and kept until process exit: init() and
+// set_device() only switch which one default_ctx() hands out, so a pointer
+// another thread obtained earlier stays valid
+std::map<std::pair<int, int>, kzgx_ctx*> g_ctxs;
 
 void check(int rc, const char* where) {
   if (rc == KZGX_OK) return;
@@ -33,8 +38,9 @@ void check(int rc, const char* where) {
 
 kzgx_ctx* default_ctx() {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_ctx) check(kzgx_create(&g_ctx, g_curve, g_device), "kzgx_create");
-  return g_ctx;
+  kzgx_ctx*& c = g_ctxs[{g_curve, g_device}];
+  if (!c) check(kzgx_create(&c, g_curve, g_device), "kzgx_create");
+  return c;
 }
 
 // r as 64-bit limbs for the selected curve
@@ -224,10 +230,6 @@ void init() { init(KZGX_CURVE_BN254); }
 void init(int curve) {
   if (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) throw std::invalid_argument("unknown curve");
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_ctx && curve != g_curve) {
-    kzgx_destroy(g_ctx);
-    g_ctx = nullptr;
-  }
   g_curve = curve;
   CURVE_ORDER_BYTES = 32;  // NumBytes(r) on both curves (trusted_setup.cpp:18)
 }
@@ -237,10 +239,6 @@ int curve() { return g_curve; }
 void set_device(int device) {
   if (device < 0) throw std::invalid_argument("negative device ordinal");
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_ctx && device != g_device) {
-    kzgx_destroy(g_ctx);
-    g_ctx = nullptr;
-  }
   g_device = device;
 }
 
@@ -619,6 +617,13 @@ std::vector<G1> trusted_setup::g1_points() const {
 void trusted_setup::precompute(int window_bits, size_t points) {
   check(kzgx_set_fixed_base(ctx, window_bits, window_bits ? (points ? std::min(points, n) : n) : 0),
         "kzgx_set_fixed_base");
+}
+
+int trusted_setup::precompute_budget(size_t budget_bytes, size_t points) {
+  int c = 0;
+  check(kzgx_set_fixed_base_budget(ctx, budget_bytes, points ? std::min(points, n) : n, &c),
+        "kzgx_set_fixed_base_budget");
+  return c;
 }
 
 std::vector<G2> trusted_setup::g2_points() const {

@@ -5,6 +5,8 @@
 // kzgx_create fails with KZGX_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <array>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -243,6 +245,45 @@ int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* 
   return KZGX_OK;
 }
 
+int kzgx_fixed_base_bytes(int curve, int c, size_t n_points, size_t* bytes) {
+  if (!bytes || (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) || !kzgx::fixed_bits_supported(c))
+    return KZGX_ERR_ARG;
+  *bytes = kzgx::fixed_table_bytes(curve, c, n_points);
+  return KZGX_OK;
+}
+
+int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_points, int* c_out) {
+  KZGX_TRY(activate(ctx));
+  if (!c_out || n_points == 0) return KZGX_ERR_ARG;
+  *c_out = 0;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  kzgx::fixed_free(&ctx->c);  // the old table's memory counts as free
+  size_t free_b = 0, total_b = 0;
+  KZGX_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
+  const size_t margin = (size_t)4 << 30;
+  const size_t avail = free_b > margin ? free_b - margin : 0;
+  const size_t cap = budget_bytes < avail ? budget_bytes : avail;
+  for (int c = 17; c >= 7; c--) {
+    if (kzgx::fixed_table_bytes(ctx->c.curve, c, n_points) > cap) continue;
+    const int rc = kzgx_set_fixed_base(ctx, c, n_points);
+    if (rc == KZGX_OK) {
+      *c_out = c;
+      return KZGX_OK;
+    }
+    if (rc != KZGX_ERR_OOM) return rc;
+  }
+  ctx->c.fixed.c_req = 0;
+  ctx->c.fixed.n_req = 0;
+  return KZGX_OK;
+}
+
+int kzgx_microbench_mad_u64(kzgx_ctx* ctx, double* lane_ops_per_s) {
+  KZGX_TRY(activate(ctx));
+  if (!lane_ops_per_s) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return kzgx::microbench_mad_u64(&ctx->c, lane_ops_per_s);
+}
+
 int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s) {
   KZGX_TRY(activate(ctx));
   if (!adds_per_s) return KZGX_ERR_ARG;
@@ -407,6 +448,14 @@ int kzgx_prove_range(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint
   while (n > 0 && (coeffs[4 * (n - 1)] | coeffs[4 * (n - 1) + 1] | coeffs[4 * (n - 1) + 2] | coeffs[4 * (n - 1) + 3]) == 0)
     n--;  // NTL keeps polynomials normalized
   if (n > len && n - len > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  {
+    // repeated points: the reference's interpolation (NTL polyfit) fails on
+    // them, so does this call (P div Z alone would still be defined)
+    std::vector<std::array<uint64_t, 4>> sorted(len);
+    for (size_t i = 0; i < len; i++) sorted[i] = {xs[4 * i + 3], xs[4 * i + 2], xs[4 * i + 1], xs[4 * i]};
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return KZGX_ERR_DIV_ZERO;
+  }
   hipStream_t st = ctx->c.stream;
   kzgx::MsmWs* ws = ctx->c.ws_for(st);
   if (!ws) return KZGX_ERR_ARG;
@@ -879,9 +928,10 @@ int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const in
 
 // Debug only (not part of include/kzg_gpu.h): copy a Pippenger workspace
 // buffer of the context's default stream to the host, after a device sync.
+// Looks the workspace up without binding or refreshing one.
 extern "C" int kzgx_debug_ws_read(kzgx_ctx* ctx, const char* name, void* host, size_t bytes) {
   KZGX_TRY(activate(ctx));
-  kzgx::MsmWs* w = ctx->c.ws_for(ctx->c.stream);
+  kzgx::MsmWs* w = ctx->c.ws_find(ctx->c.stream);
   if (!w || !name || !host) return KZGX_ERR_ARG;
   const void* src = nullptr;
   size_t cap = 0;

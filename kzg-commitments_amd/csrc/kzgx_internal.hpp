@@ -83,15 +83,23 @@ struct Ctx {
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];
   FixedTable fixed;
-  // the workspace bound to stream st (claimed on first use).  With more
-  // than KZGX_MAX_STREAMS distinct streams the least recently bound slot is
-  // rebound after a device synchronisation (its previous owner's work has
-  // then finished, so nothing still reads the buffers); nullptr only if that
-  // synchronisation fails.
+  // the workspace bound to stream st (claimed on first use; every lookup
+  // refreshes its use stamp).  With more than KZGX_MAX_STREAMS distinct
+  // streams the least recently USED slot is rebound after its previous
+  // owner stream has drained (hipStreamSynchronize of that stream only:
+  // other streams and contexts keep running; a stream must outlive the
+  // calls made on it); nullptr only if that synchronisation fails.
   uint64_t ws_clock = 0;
-  MsmWs* ws_for(hipStream_t st) {
+  MsmWs* ws_find(hipStream_t st) {
     for (auto& w : ws)
       if (w.used && w.owner == st) return &w;
+    return nullptr;
+  }
+  MsmWs* ws_for(hipStream_t st) {
+    if (MsmWs* w = ws_find(st)) {
+      w->bound_at = ++ws_clock;
+      return w;
+    }
     for (auto& w : ws)
       if (!w.used) {
         w.used = true;
@@ -102,7 +110,7 @@ struct Ctx {
     MsmWs* lru = &ws[0];
     for (auto& w : ws)
       if (w.bound_at < lru->bound_at) lru = &w;
-    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    if (hipStreamSynchronize(lru->owner) != hipSuccess) return nullptr;
     lru->owner = st;
     lru->bound_at = ++ws_clock;
     return lru;
@@ -155,6 +163,8 @@ int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
 // mixed additions / s of the fixed-base accumulation loop on L1-resident operands (msm_fixed.hip)
 int microbench_mixed_add(Ctx* ctx, double* rate);
+int microbench_mad_u64(Ctx* ctx, double* rate);
+size_t fixed_table_bytes(int curve, int c, size_t n);
 int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res);  // ns, core clocks per op
 // one workgroup sums count XYZZ points -> canonical affine (msm.hip)
 int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);

@@ -29,103 +29,14 @@
 #include <algorithm>
 
 #include "curve.hpp"
+#include "fixed_accum.hpp"
 #include "kzgx_internal.hpp"
 
 namespace kzgx {
 
-// Table point layout, per curve (KZGX_FIXED_L29 = 0 / 1 forces one for both):
-//  * packed: x || y as canonical-width 32-bit words, 64 B (BN254) / 96 B
-//    (BLS12-381), unpacked to radix-2^29 limbs per term;
-//  * radix-2^29: the limbs the accumulation consumes, padded to 80 B / 112 B.
-// Measured on MI355X (profiles/r02_pmc_fetch_calibration.json): every DRAM
-// read is a 128-B request; an 80-B BN254 entry costs 1.5 lines and a 64-B
-// one exactly one, so packed moves 33% fewer bytes (8.7 vs 13.0 GB per
-// 1024-MSM launch), needs 20% less HBM and is 1% faster -- and lets c = 17
-// (15 windows) fit.  BLS12-381 keeps the radix-2^29 entries: its 14-limb
-// unpack does not hide, 112-B entries are 2% faster than 96-B ones
-// (profiles/r02_ab_table_layout.json).
-template <class C>
-constexpr bool fixed_l29() {
-#ifdef KZGX_FIXED_L29
-  return KZGX_FIXED_L29 != 0;
-#else
-  return C::Fp29::L > 9;
-#endif
-}
-template <class C>
-constexpr int packed_words() {
-  return fixed_l29<C>() ? affine_words<C>() : 2 * C::Fp::N;
-}
-
-template <class C, int CB>
-struct FixedWin {
-  // signed digits of a scalar < r need W c >= bits(r) + 1: the top digit
-  // then absorbs the final carry without overflowing H
-  static constexpr int W = (C::SCALAR_BITS + 1 + CB - 1) / CB;
-  static constexpr uint32_t H = 1u << (CB - 1);
-};
-
 int fixed_windows(int curve, int c) {
   const int bits = curve == KZGX_CURVE_BN254 ? BN254G1::SCALAR_BITS : BLS12381G1::SCALAR_BITS;
   return (bits + 1 + c - 1) / c;
-}
-
-template <class C>
-KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
-  if (fixed_l29<C>()) return affine_load<C>(p);
-  using F = typename C::Fp29;
-  constexpr int N = C::Fp::N;
-  uint32_t wx[N], wy[N];
-#pragma unroll
-  for (int k = 0; k < N / 4; k++) {
-    uint4 a = reinterpret_cast<const uint4*>(p)[k];
-    uint4 b = reinterpret_cast<const uint4*>(p + N)[k];
-    wx[4 * k] = a.x; wx[4 * k + 1] = a.y; wx[4 * k + 2] = a.z; wx[4 * k + 3] = a.w;
-    wy[4 * k] = b.x; wy[4 * k + 1] = b.y; wy[4 * k + 2] = b.z; wy[4 * k + 3] = b.w;
-  }
-  Affine<C> r;
-  r.x = f29_from_words<F, N>(wx);
-  r.y = f29_from_words<F, N>(wy);
-  return r;
-}
-
-template <class C>
-KZGX_DEV void packed_store(uint32_t* __restrict__ p, const Affine<C>& a) {
-  if (fixed_l29<C>()) {
-    affine_store<C>(p, a);
-    return;
-  }
-  using F = typename C::Fp29;
-  constexpr int N = C::Fp::N;
-  uint32_t wx[N], wy[N];
-  f29_to_words<F, N>(a.x, wx);
-  f29_to_words<F, N>(a.y, wy);
-#pragma unroll
-  for (int k = 0; k < N / 4; k++) {
-    reinterpret_cast<uint4*>(p)[k] = make_uint4(wx[4 * k], wx[4 * k + 1], wx[4 * k + 2], wx[4 * k + 3]);
-    reinterpret_cast<uint4*>(p + N)[k] = make_uint4(wy[4 * k], wy[4 * k + 1], wy[4 * k + 2], wy[4 * k + 3]);
-  }
-}
-
-// s mod r for any 256-bit s (the ABI asks for canonical scalars; this keeps a
-// non-canonical one exact for points of order r instead of overflowing the
-// top digit).  Common case: one compare of the top word.
-template <class C>
-KZGX_DEV void scalar_reduce(uint32_t (&s)[8]) {
-  using R = typename C::Fr;
-  while (s[7] >= R::P[7]) {
-    uint32_t d[8];
-    int64_t br = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      int64_t v = (int64_t)s[k] - (int64_t)R::P[k] + br;
-      d[k] = (uint32_t)v;
-      br = v >> 32;
-    }
-    if (br < 0) break;  // s < r
-#pragma unroll
-    for (int k = 0; k < 8; k++) s[k] = d[k];
-  }
 }
 
 // --------------------------------------------------------------------------
@@ -184,136 +95,6 @@ __global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restri
     xyzz_to_affine<C>(acc, a);  // (k0 + j) B != O since k0 + j <= H < r
     packed_store<C>(out + (size_t)j * PW, a);
   }
-}
-
-// --------------------------------------------------------------------------
-// MSM
-// --------------------------------------------------------------------------
-// shift the 256-bit scalar right by CB (static register indexing only)
-template <int CB>
-KZGX_DEV void shr_scalar(uint32_t (&s)[8]) {
-#pragma unroll
-  for (int k = 0; k < 7; k++) s[k] = __builtin_amdgcn_alignbit(s[k + 1], s[k], CB);
-  s[7] >>= CB;
-}
-
-// next signed digit from the low CB bits of s (consumed), carry in/out
-template <int CB>
-KZGX_DEV int next_digit(uint32_t (&s)[8], uint32_t& carry) {
-  uint32_t raw = (s[0] & ((1u << CB) - 1u)) + carry;
-  shr_scalar<CB>(s);
-  carry = raw > (1u << (CB - 1)) ? 1u : 0u;
-  return (int)raw - (int)(carry << CB);
-}
-
-// thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
-// (a wavefront reads 64 consecutive scalars per point step)
-template <class C>
-struct PackedPt {
-  uint4 q[packed_words<C>() / 4];
-};
-
-template <class C>
-KZGX_DEV PackedPt<C> packed_fetch(const uint32_t* __restrict__ p) {
-  PackedPt<C> r;
-#pragma unroll
-  for (int k = 0; k < packed_words<C>() / 4; k++) r.q[k] = reinterpret_cast<const uint4*>(p)[k];
-  return r;
-}
-
-template <class C>
-KZGX_DEV Affine<C> packed_unpack(const PackedPt<C>& r) {
-  using F = typename C::Fp29;
-  Affine<C> a;
-  if (fixed_l29<C>()) {
-    constexpr int L = F::L;
-    uint32_t w[packed_words<C>()];
-#pragma unroll
-    for (int k = 0; k < packed_words<C>() / 4; k++) {
-      w[4 * k] = r.q[k].x; w[4 * k + 1] = r.q[k].y; w[4 * k + 2] = r.q[k].z; w[4 * k + 3] = r.q[k].w;
-    }
-#pragma unroll
-    for (int i = 0; i < L; i++) {
-      a.x.v[i] = w[i];
-      a.y.v[i] = w[L + i];
-    }
-    return a;
-  }
-  constexpr int N = C::Fp::N;
-  uint32_t wx[N], wy[N];
-#pragma unroll
-  for (int k = 0; k < N / 4; k++) {
-    const uint4 p = r.q[k], q = r.q[N / 4 + k];
-    wx[4 * k] = p.x; wx[4 * k + 1] = p.y; wx[4 * k + 2] = p.z; wx[4 * k + 3] = p.w;
-    wy[4 * k] = q.x; wy[4 * k + 1] = q.y; wy[4 * k + 2] = q.z; wy[4 * k + 3] = q.w;
-  }
-  a.x = f29_from_words<F, N>(wx);
-  a.y = f29_from_words<F, N>(wy);
-  return a;
-}
-
-// waves per SIMD the accumulation kernel is register-budgeted for
-#ifndef KZGX_FIXED_WAVES_BN
-#define KZGX_FIXED_WAVES_BN 3
-#endif
-#ifndef KZGX_FIXED_WAVES_BLS
-#define KZGX_FIXED_WAVES_BLS 2
-#endif
-template <class C>
-constexpr int fixed_accum_waves() {
-  return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : KZGX_FIXED_WAVES_BLS;
-}
-
-// thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
-// (a wavefront reads 64 consecutive scalars per point step)
-template <class C, int CB>
-__global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
-    const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
-    uint32_t n_t, const uint8_t* __restrict__ inf, uint32_t T, uint32_t* __restrict__ part) {
-  constexpr int PW = packed_words<C>();
-  constexpr int XW = xyzz_words<C>();
-  constexpr int W = FixedWin<C, CB>::W;
-  constexpr uint32_t H = FixedWin<C, CB>::H;
-  const uint32_t b = blockIdx.y;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
-  const uint32_t* sc = scalars + (size_t)b * stride_words;
-  const size_t wstride = (size_t)n_t * H * PW;  // words between windows
-  Xyzz<C> acc = xyzz_inf<C>();
-  for (uint32_t i = t; i < n; i += T) {
-    if (inf[i]) continue;
-    uint32_t s[8];
-    {
-      uint4 lo = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[0];
-      uint4 hi = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[1];
-      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
-      s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
-    }
-    scalar_reduce<C>(s);
-    const uint32_t* base = tab + (size_t)i * H * PW;
-    uint32_t carry = 0;
-    // software pipeline: the (packed) lookup of term w + 1 is in flight
-    // during the mixed addition of term w
-    int d = next_digit<CB>(s, carry);
-    PackedPt<C> nx = packed_fetch<C>(base + (size_t)((d < 0 ? -d : d) - (d != 0)) * PW);
-#pragma unroll 1
-    for (int w = 0; w < W; w++) {
-      Affine<C> cur = packed_unpack<C>(nx);
-      int dn = 0;
-      if (w + 1 < W) {
-        dn = next_digit<CB>(s, carry);
-        nx = packed_fetch<C>(base + (size_t)(w + 1) * wstride + (size_t)((dn < 0 ? -dn : dn) - (dn != 0)) * PW);
-      }
-      if (d != 0) {
-        // -T = (x, 2m - y): one v_sub per limb (f29_neg_lazy; the
-        // mixed add only multiplies y and feeds it to carry-absorbing subs)
-        if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
-        acc = xyzz_add_affine_impl<C>(acc, cur);
-      }
-      d = dn;
-    }
-  }
-  xyzz_store<C>(part + ((size_t)b * T + t) * XW, acc);
 }
 
 // one wavefront per MSM: strided sums of the T partials, then a shuffle tree
@@ -781,6 +562,12 @@ static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t bat
   }
 }
 
+size_t fixed_table_bytes(int curve, int c, size_t n) {
+  if (c <= 0) return 0;
+  const size_t pb = curve == KZGX_CURVE_BN254 ? packed_words<BN254G1>() * 4 : packed_words<BLS12381G1>() * 4;
+  return (size_t)fixed_windows(curve, c) * n * ((size_t)1 << (c - 1)) * pb;
+}
+
 bool fixed_bits_supported(int c) {
   return c == 0 || c == 4 || (c >= 7 && c <= 17);
 }
@@ -858,6 +645,55 @@ static int microbench_madd_impl(Ctx* ctx, double* rate) {
   KZGX_TRY_HIP(e);
   KZGX_TRY_HIP(hipGetLastError());
   *rate = (double)waves * 64 * iters / (ms * 1e-3);
+  return KZGX_OK;
+}
+
+// v_mad_u64_u32 issue ceiling: 8 independent accumulator chains per lane,
+// 256 mads per chain per iteration, 8 waves per SIMD (the instruction
+// exactly, in asm; scripts/micro_valu.hip, profiles/r01_micro_valu.txt)
+__global__ __launch_bounds__(256) void k_microbench_mad64(uint32_t iters, uint32_t* __restrict__ sink) {
+  uint64_t acc[8];
+  const uint32_t a = threadIdx.x + 1, b = blockIdx.x + 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) acc[k] = k;
+#pragma unroll 1
+  for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        uint64_t sc;
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(sc) : "v"(a), "v"(b));
+      }
+    }
+  }
+  uint64_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) o ^= acc[k];
+  if ((uint32_t)o == 0x9e3779b9u) sink[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)o;
+}
+
+int microbench_mad_u64(Ctx* ctx, double* rate) {
+  hipStream_t st = ctx->stream;
+  const uint32_t blocks = 256 * 8, iters = 64;
+  uint32_t* d_sink = nullptr;
+  KZGX_TRY_HIP(hipMalloc((void**)&d_sink, (size_t)blocks * 256 * 4));
+  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, 2u, d_sink);  // warm
+  hipEvent_t a, b;
+  KZGX_TRY_HIP(hipEventCreate(&a));
+  KZGX_TRY_HIP(hipEventCreate(&b));
+  KZGX_TRY_HIP(hipEventRecord(a, st));
+  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, iters, d_sink);
+  KZGX_TRY_HIP(hipEventRecord(b, st));
+  KZGX_TRY_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  hipError_t e = hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(d_sink);
+  KZGX_TRY_HIP(e);
+  KZGX_TRY_HIP(hipGetLastError());
+  *rate = (double)blocks * 256 * iters * 256 / (ms * 1e-3);
   return KZGX_OK;
 }
 

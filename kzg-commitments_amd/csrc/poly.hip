@@ -578,6 +578,20 @@ static uint32_t* vanishing_mont(const uint32_t* d_x, size_t n, uint32_t* ws, hip
 // every step two truncated products of one wavefront per output coefficient
 // (BN254's r - 1 has 2-adicity 2: no NTT domain, and at these sizes the
 // parallel schoolbook products are a fraction of the MSM anyway).
+//
+// For few points on a long polynomial the Newton route costs ~1.8 m^2
+// products while dividing by the len linear factors one after the other
+// (floor division by monic factors composes: P div (X - x_0) div (X - x_1)
+// ... = P div Z) costs len synthetic divisions of O(n) each, on the chip-wide
+// single-opening quotient (quotient_single_impl: k_qbig_* from 2^13
+// coefficients).  The division chain is sequential, so Newton (fully
+// parallel) stays for len comparable to m.
+template <class FR>
+static bool prove_range_by_division(size_t n, size_t len) {
+  const size_t m = n - len;
+  return len <= 4 || (double)m * (double)m > 64.0 * (double)len * (double)n;
+}
+
 template <class FR>
 static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_x, size_t len,
                                  uint32_t* d_q, size_t* nq_out, hipStream_t st) {
@@ -586,6 +600,21 @@ static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const 
   *nq_out = 0;
   if (n <= len) return KZGX_OK;  // deg P < len: I = P, q = 0 (NTL normalizes to the zero polynomial)
   const size_t m = n - len;
+  if (prove_range_by_division<FR>(n, len)) {
+    // ping-pong between d_q and a scratch buffer, ending in d_q
+    KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (n - 1) * eb, &ctx->poly_ws2_b));
+    uint32_t* tmp = (uint32_t*)ctx->d_poly_ws2;
+    const uint32_t* cur = d_P;
+    size_t ncur = n;
+    for (size_t i = 0; i < len; i++) {
+      uint32_t* dst = ((len - 1 - i) & 1) ? tmp : d_q;
+      KZGX_TRY(quotient_single_impl<FR>(ctx, cur, ncur, 0, d_x + i * N, 1, dst, 0, nullptr, st));
+      cur = dst;
+      ncur--;
+    }
+    *nq_out = m;
+    return KZGX_OK;
+  }
   // workspace: tree (len + 2 (2 len + 2)), Rz, S, E, Prev, Qrev (m each)
   const size_t tree = len + 2 * (2 * len + 2);
   KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (tree + 5 * m) * eb, &ctx->poly_ws2_b));

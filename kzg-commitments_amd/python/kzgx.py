@@ -22,7 +22,8 @@ BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
-    "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
+    "kzgx_microbench_mad_u64", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device",
@@ -76,6 +77,9 @@ def lib():
             "kzgx_set_segment": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_set_fixed_base": (ctypes.c_int, [vp, ctypes.c_int, sz]),
             "kzgx_fixed_base_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+            "kzgx_fixed_base_bytes": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, sz, ctypes.POINTER(sz)]),
+            "kzgx_set_fixed_base_budget": (ctypes.c_int, [vp, sz, sz, intp]),
+            "kzgx_microbench_mad_u64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_microbench_mixed_add": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
@@ -143,6 +147,13 @@ def msm_g1_sharded(ctxs, starts, scalars):
     return out, bool(oi.value)
 
 
+def fixed_base_bytes(curve: str, c: int, n_points: int) -> int:
+    """device bytes of a fixed-base table (host arithmetic, no device)"""
+    b = sz(0)
+    _chk(lib().kzgx_fixed_base_bytes(CURVES[curve], c, n_points, ctypes.byref(b)), "kzgx_fixed_base_bytes")
+    return b.value
+
+
 class Context:
     """One device context (SRS + stream + workspaces), kzgx_ctx*."""
 
@@ -198,6 +209,20 @@ class Context:
         _chk(lib().kzgx_fixed_base_info(self.h, ctypes.byref(c), ctypes.byref(n), ctypes.byref(b)),
              "kzgx_fixed_base_info")
         return c.value, n.value, b.value
+
+    def set_fixed_base_budget(self, budget_bytes: int, n_points: int) -> int:
+        """widest table window whose table fits budget_bytes and free device
+        memory (0: none built, Pippenger); returns the window built"""
+        c = ctypes.c_int(0)
+        _chk(lib().kzgx_set_fixed_base_budget(self.h, int(budget_bytes), n_points, ctypes.byref(c)),
+             "kzgx_set_fixed_base_budget")
+        return c.value
+
+    def microbench_mad_u64(self) -> float:
+        """v_mad_u64_u32 lane operations / s (hardware issue ceiling)"""
+        r = ctypes.c_double(0)
+        _chk(lib().kzgx_microbench_mad_u64(self.h, ctypes.byref(r)), "kzgx_microbench_mad_u64")
+        return r.value
 
     def set_fixed_points_per_thread(self, p: int):
         _chk(lib().kzgx_set_fixed_points_per_thread(self.h, p), "kzgx_set_fixed_points_per_thread")

@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Count the VALU instructions of a kernel's hot loop in gfx950 assembly.
+
+    hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S -o x.s csrc/msm_fixed.hip
+    python3 scripts/isa_count.py x.s 'k_fixed_accumINS_7BN254G1ELi17E' [--per N]
+
+Finds the kernel whose symbol contains the given substring, then the loop
+(a backward branch to an earlier label) holding the most v_mad_u64_u32, and
+prints a histogram of the instructions between that label and the branch.
+Loop bodies of the accumulation kernels hold one mixed addition on the common
+path plus the rare special cases (doubling, infinity), so the script also
+reports the counts of the straight-line blocks on the fall-through path
+(`--path`): from the loop head, follow fall-through and forward branches'
+not-taken edges to the back edge.  --per N divides the totals by N (e.g. the
+number of mixed additions per iteration).
+
+Used for bench.py's secondary.mad_issue (v_mad_u64_u32 per mixed addition)
+and DESIGN.md section 7.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import re
+import sys
+
+LABEL = re.compile(r"^(\.LBB\d+_\d+|\.L[\w$.]+):")
+BRANCH = re.compile(r"^\s*(s_cbranch_\w+|s_branch)\s+(\.LBB\d+_\d+)")
+
+
+def kernel_body(lines, needle):
+    start = None
+    for i, ln in enumerate(lines):
+        if start is None:
+            m = re.match(r"^([A-Za-z_][\w$.]*):", ln)
+            if m and needle in m.group(1):
+                start = i
+        elif ln.startswith(".Lfunc_end"):
+            return lines[start:i]
+    if start is None:
+        raise SystemExit("kernel with %r not found" % needle)
+    return lines[start:]
+
+
+def mnemonic(ln):
+    s = ln.strip()
+    if not s or s.startswith(";") or s.startswith(".") or s.endswith(":"):
+        return None
+    return s.split()[0]
+
+
+def histogram(body):
+    h = collections.Counter()
+    for ln in body:
+        m = mnemonic(ln)
+        if m:
+            h[m] += 1
+    return h
+
+
+def hot_loop(body):
+    labels = {}
+    for i, ln in enumerate(body):
+        m = LABEL.match(ln)
+        if m:
+            labels[m.group(1)] = i
+    best = None
+    for i, ln in enumerate(body):
+        m = BRANCH.match(ln)
+        if m and m.group(2) in labels and labels[m.group(2)] < i:
+            lo = labels[m.group(2)]
+            mads = sum(1 for x in body[lo:i] if "v_mad_u64_u32" in x)
+            if best is None or mads > best[0]:
+                best = (mads, lo, i)
+    if best is None:
+        raise SystemExit("no loop found")
+    return best[1], best[2]
+
+
+def fallthrough_path(body, lo, hi):
+    """instructions on the not-taken path of every forward conditional branch
+    from the loop head to the back edge (unconditional forward jumps are
+    followed)"""
+    labels = {}
+    for i in range(lo, hi + 1):
+        m = LABEL.match(body[i])
+        if m:
+            labels[m.group(1)] = i
+    out = []
+    i = lo
+    seen = set()
+    while i <= hi and i not in seen:
+        seen.add(i)
+        ln = body[i]
+        m = BRANCH.match(ln)
+        if m and m.group(1) == "s_branch" and m.group(2) in labels and labels[m.group(2)] > i:
+            i = labels[m.group(2)]
+            continue
+        out.append(ln)
+        i += 1
+    return out
+
+
+VALU_PREFIX = "v_"
+
+
+def summarize(h, per):
+    valu = sum(v for k, v in h.items() if k.startswith(VALU_PREFIX))
+    res = {
+        "v_mad_u64_u32": h.get("v_mad_u64_u32", 0) / per,
+        "valu": valu / per,
+        "salu": sum(v for k, v in h.items() if k.startswith("s_")) / per,
+        "top": {k: v / per for k, v in h.most_common(24)},
+    }
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("asm")
+    ap.add_argument("kernel")
+    ap.add_argument("--per", type=float, default=1.0)
+    ap.add_argument("--json", action="store_true")
+    a = ap.parse_args()
+    with open(a.asm) as f:
+        lines = f.read().splitlines()
+    body = kernel_body(lines, a.kernel)
+    lo, hi = hot_loop(body)
+    loop = body[lo:hi + 1]
+    path = fallthrough_path(body, lo, hi)
+    out = {"kernel": a.kernel, "loop_lines": hi - lo, "loop": summarize(histogram(loop), a.per),
+           "path": summarize(histogram(path), a.per)}
+    if a.json:
+        print(json.dumps(out))
+    else:
+        for k in ("loop", "path"):
+            s = out[k]
+            print("%s: v_mad_u64_u32 %.0f  VALU %.0f  SALU %.0f" % (k, s["v_mad_u64_u32"], s["valu"], s["salu"]))
+            print("   ", ", ".join("%s %.0f" % kv for kv in s["top"].items()))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

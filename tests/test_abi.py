@@ -59,3 +59,16 @@ def test_bad_arguments_rejected_before_device():
     h = ctypes.c_void_p()
     assert kzgx.lib().kzgx_create(ctypes.byref(h), 9, 0) == -1  # unknown curve
     assert kzgx.lib().kzgx_create(None, 0, 0) == -1
+
+
+def test_fixed_base_bytes_matches_the_table_layout():
+    """kzgx_fixed_base_bytes (host arithmetic, no device): W x n x 2^(c-1)
+    entries of 64 B (BN254) / 112 B (BLS12-381), W = ceil((bits(r)+1)/c) --
+    the sizes include/kzg.h quotes"""
+    import kzgx
+    assert kzgx.fixed_base_bytes("BN254", 17, 4097) == 15 * 4097 * (1 << 16) * 64      # 257.8 GB
+    assert kzgx.fixed_base_bytes("BN254", 16, 4097) == 16 * 4097 * (1 << 15) * 64      # 137.5 GB
+    assert kzgx.fixed_base_bytes("BN254", 12, 4097) == 22 * 4097 * (1 << 11) * 64      # 11.8 GB
+    assert kzgx.fixed_base_bytes("BLS12381", 16, 4097) == 16 * 4097 * (1 << 15) * 112  # 240.6 GB
+    with pytest.raises(kzgx.KzgxError):
+        kzgx.fixed_base_bytes("BN254", 18, 4097)

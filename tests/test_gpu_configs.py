@@ -1,14 +1,13 @@
 """GPU parity at the BASELINE.json configurations and at the exact kernel
 instantiations the headline bench runs.
 
-  * configs[1] / bench.py default: degree-4096 BN254 commits + single-opening
-    proofs, batch 1024, fixed-base table c = 16 (k_fixed_accum<BN254G1, 16>),
-    16 points per thread, commits and proofs on two streams sharing one
-    context;
-  * configs[2]: one degree-4096 polynomial opened at x = 0..4095 as ONE
-    4096-wide batch, on the c = 16 table and on Pippenger; plus the
-    reference-semantics multi-proof create_proof(poly, 0, N) of
-    benchmark/benchmark.cpp:73-82 for N in {128, 2048, 4096};
+  * every throughput line of bench.py (configs[1] cfg2, configs[2] cfg3,
+    configs[3] cfg4) at its exact launch shape (bench.WORKLOAD_SHAPES: curve,
+    window, batch, points per thread, streams), through the bench's own step
+    and checker, every output checked;
+  * configs[2] on Pippenger too, plus the reference-semantics multi-proof
+    create_proof(poly, 0, N) of benchmark/benchmark.cpp:73-82 for N in
+    {128, 2048, 4096};
   * configs[4]: one 2^20 + 1 coefficient commitment (chunked Pippenger), and
     the same commitment sharded over 2 and 8 contexts (kzgx_msm_g1_sharded);
   * the c = 16 / 17 window instantiations on both curves against the naive
@@ -86,106 +85,88 @@ def test_headline_window_bits(name, C, c):
         ctx.close()
 
 
-@pytest.fixture(scope="module")
-def bn254_c16():
-    """the bench's context: BN254, SRS 5000 from the fixed tau, c = 16 table
-    over the 4097-point prefix (171.8 GB), 16 points per thread"""
-    import kzgx
-    C = K.BN254
-    ctx = kzgx.Context("BN254")
-    ctx.gen_srs(K.default_tau(C), 5000)
-    ctx.set_fixed_base(16, 4097)
-    ctx.set_fixed_points_per_thread(16)
-    assert ctx.fixed_base_info()[:2] == (16, 4097)
-    yield ctx
-    ctx.close()
-
-
 def _proof_scalar(C, tau, ptau, pz, z):
     return (ptau - pz) * pow((tau - z) % C.r, -1, C.r) % C.r
 
 
-def test_bench_shape_two_streams(bn254_c16):
-    """bench.py's default step, exactly: 1024 commits (n = 4097) on one
-    stream and 1024 single-opening proofs (n = 4097, z = b) on another, both
-    on one context's c = 16 table; every one of the 2048 results checked."""
-    import corc
+def _bench():
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    return bench
+
+
+@pytest.mark.parametrize("workload", ["cfg2", "cfg3", "cfg4"])
+def test_bench_shape(workload):
+    """each throughput line of bench.py exactly as it runs: the curve, window,
+    batch, points per thread and streams of bench.WORKLOAD_SHAPES, the
+    bench's own inputs and step (bench.make_step: commits and proofs on two
+    streams of one context), run twice (the second pass reuses the per-stream
+    workspaces), then EVERY output checked with bench.check_step (commit =
+    [P(tau)]G1, proof = [q(tau)]G1, y = P(z)).  One table at a time: the
+    BN254 c = 17 table is 257.8 GB, the BLS12-381 c = 16 one 240.6 GB."""
     import torch
-    name, C = "BN254", K.BN254
-    ctx = bn254_c16
-    tau = K.default_tau(C)
-    n, B = 4097, 1024
-    rng = np.random.default_rng(0x4B5A47)
-    coeffs = rng.integers(0, 2**63, size=(B, n, 4), dtype=np.uint64)
-    coeffs[..., 3] &= np.uint64((1 << 59) - 1)  # < 2^251 < r: canonical
-    coeffs[3] = 0                                # zero polynomial -> infinity
-    coeffs[5, 1:] = 0                            # constant polynomial
-    zs = np.zeros((B, 4), dtype=np.uint64)
-    zs[:, 0] = np.arange(B, dtype=np.uint64)
-    dev = torch.device("cuda", 0)
-    d_c = torch.from_numpy(coeffs.view(np.int64)).to(dev)
-    d_z = torch.from_numpy(zs.view(np.int64)).to(dev)
-    d_co = torch.zeros((B, 8), dtype=torch.int64, device=dev)
-    d_ci = torch.zeros((B,), dtype=torch.int32, device=dev)
-    d_po = torch.zeros((B, 8), dtype=torch.int64, device=dev)
-    d_pi = torch.zeros((B,), dtype=torch.int32, device=dev)
-    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-    torch.cuda.synchronize(dev)
-    for _ in range(2):  # twice: the second pass reuses the per-stream workspaces
-        ctx.prove_single_batch_device(d_c.data_ptr(), n, n, d_z.data_ptr(), B, d_po.data_ptr(), d_pi.data_ptr(),
-                                      None, s2.cuda_stream)
-        ctx.msm_batch_device(d_c.data_ptr(), n, B, n, d_co.data_ptr(), d_ci.data_ptr(), s1.cuda_stream)
-    torch.cuda.synchronize(dev)
-    co, ci = d_co.cpu().numpy().view(np.uint64), d_ci.cpu().numpy()
-    po, pi = d_po.cpu().numpy().view(np.uint64), d_pi.cpu().numpy()
-    for b in range(B):
-        ptau = corc.poly_eval(name, coeffs[b], tau)
-        assert pt(name, co[b], ci[b]) == g_mul(name, C, ptau), ("commit", b)
-        pz = corc.poly_eval(name, coeffs[b], b)
-        assert pt(name, po[b], pi[b]) == g_mul(name, C, _proof_scalar(C, tau, ptau, pz, b)), ("proof", b)
-
-
-def _cfg3_check(name, C, ctx, tau):
-    import corc
-    import torch
-    n = 4097
-    coeffs = limbs(K.random_scalars(C, n, seed=0xCF63))
-    B = 4096
-    zs = np.zeros((B, 4), dtype=np.uint64)
-    zs[:, 0] = np.arange(B, dtype=np.uint64)
-    dev = torch.device("cuda", 0)
-    d_c = torch.from_numpy(coeffs.view(np.int64)).to(dev)
-    d_z = torch.from_numpy(zs.view(np.int64)).to(dev)
-    d_po = torch.zeros((B, 8), dtype=torch.int64, device=dev)
-    d_pi = torch.zeros((B,), dtype=torch.int32, device=dev)
-    d_y = torch.zeros((B, 4), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize(dev)
-    ctx.prove_single_batch_device(d_c.data_ptr(), n, 0, d_z.data_ptr(), B, d_po.data_ptr(), d_pi.data_ptr(),
-                                  d_y.data_ptr(), ctx.stream)
-    ctx.sync()
-    po, pi = d_po.cpu().numpy().view(np.uint64), d_pi.cpu().numpy()
-    ys = corc.limbs_to_ints(d_y.cpu().numpy().view(np.uint64))
-    ptau = corc.poly_eval(name, coeffs, tau)
-    for z in range(B):
-        pz = corc.poly_eval(name, coeffs, z)
-        assert ys[z] == pz, ("y", z)
-        assert pt(name, po[z], pi[z]) == g_mul(name, C, _proof_scalar(C, tau, ptau, pz, z)), ("proof", z)
-
-
-def test_cfg3_4096_openings_table(bn254_c16):
-    """configs[2]: 4096 single-point openings of one degree-4096 polynomial
-    as one batch on the c = 16 fixed-base table"""
-    _cfg3_check("BN254", K.BN254, bn254_c16, K.default_tau(K.BN254))
-
-
-def test_cfg3_4096_openings_pippenger():
-    """configs[2] on the default (table-less) Pippenger path"""
     import kzgx
+    bench = _bench()
+    shape = bench.WORKLOAD_SHAPES[workload]
+    curve = shape["curve"]
+    C = K.BN254 if curve == "BN254" else K.BLS12381
+    tau = K.default_tau(C)
+    n = bench.DEGREE + 1
+    B = shape["batch"]
+    ctx = kzgx.Context(curve)
+    try:
+        ctx.gen_srs(tau, bench.SRS_POINTS)
+        ctx.set_fixed_base(shape["fixed_bits"], n)
+        assert ctx.fixed_base_info()[:2] == (shape["fixed_bits"], n)
+        ctx.set_fixed_points_per_thread(shape["points_per_thread"])
+        coeffs, zs = bench.bench_inputs(C, workload, B, n)
+        if workload != "cfg3":
+            coeffs[3] = 0          # zero polynomial: commit and proof at infinity
+            coeffs[5, 1:] = 0      # constant polynomial: proof at infinity
+            coeffs[7, :] = coeffs[6, :]  # a repeated polynomial
+        dev = torch.device("cuda", 0)
+        bufs = bench.StepBuffers(torch, dev, coeffs, zs, ctx.w64)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        step = bench.make_step(ctx, workload, n, bufs, streams)
+        torch.cuda.synchronize(dev)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
+        checked, ok, bad = bench.check_step(curve, C, tau, workload, coeffs, zs, bufs, ctx.w64)
+        assert checked == (2 * B if workload == "cfg3" else 3 * B)
+        assert ok == checked, bad
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("workload", ["cfg2", "cfg3"])
+def test_bench_step_pippenger(workload):
+    """the same bench steps on the default (table-less) Pippenger path, what
+    create_commit / create_proof run without precompute(): every output"""
+    import torch
+    import kzgx
+    bench = _bench()
     C = K.BN254
+    tau = K.default_tau(C)
+    n = bench.DEGREE + 1
+    B = 1024 if workload == "cfg2" else 4096
     ctx = kzgx.Context("BN254")
     try:
-        ctx.gen_srs(K.default_tau(C), 5000)
-        _cfg3_check("BN254", C, ctx, K.default_tau(C))
+        ctx.gen_srs(tau, bench.SRS_POINTS)
+        coeffs, zs = bench.bench_inputs(C, workload, B, n)
+        dev = torch.device("cuda", 0)
+        bufs = bench.StepBuffers(torch, dev, coeffs, zs, ctx.w64)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        step = bench.make_step(ctx, workload, n, bufs, streams)
+        torch.cuda.synchronize(dev)
+        step()
+        torch.cuda.synchronize(dev)
+        checked, ok, bad = bench.check_step("BN254", C, tau, workload, coeffs, zs, bufs, ctx.w64)
+        assert ok == checked, bad
     finally:
         ctx.close()
 

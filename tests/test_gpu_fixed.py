@@ -220,3 +220,48 @@ def test_fixed_flat_terms(name, C, tau_kind, batch, fresh_ctx):
     out, inf = ctx.msm_batch(S, n, batch)
     for b in range(batch):
         assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+
+
+def test_fixed_base_budget_picks_the_widest_fitting_window():
+    """kzgx_set_fixed_base_budget: the widest c whose table fits the budget
+    (kzgx_fixed_base_bytes), none below c = 7 (Pippenger stays); exact MSMs
+    either way"""
+    import kzgx
+    import kzg_ref as K
+    C = K.BN254
+    tau = K.default_tau(C)
+    ctx = kzgx.Context("BN254")
+    try:
+        ctx.gen_srs(tau, 300)
+        n = 257
+        b12 = kzgx.fixed_base_bytes("BN254", 12, n)
+        b13 = kzgx.fixed_base_bytes("BN254", 13, n)
+        c = ctx.set_fixed_base_budget(b13 - 1, n)
+        assert c == 12 and ctx.fixed_base_info()[:3] == (12, n, b12)
+        P = K.random_scalars(C, n, seed=77)
+        out, inf = ctx.msm(np.array([[(v >> (64 * i)) & (2**64 - 1) for i in range(4)] for v in P], dtype=np.uint64))
+        exp = K.commit_via_tau(C, tau, P)
+        got = None if inf else (sum(int(out[i]) << (64 * i) for i in range(4)), sum(int(out[4 + i]) << (64 * i) for i in range(4)))
+        assert got == exp
+        c = ctx.set_fixed_base_budget(kzgx.fixed_base_bytes("BN254", 7, n) - 1, n)
+        assert c == 0 and ctx.fixed_base_info()[0] == 0
+        out, inf = ctx.msm(np.array([[(v >> (64 * i)) & (2**64 - 1) for i in range(4)] for v in P], dtype=np.uint64))
+        got = None if inf else (sum(int(out[i]) << (64 * i) for i in range(4)), sum(int(out[4 + i]) << (64 * i) for i in range(4)))
+        assert got == exp
+    finally:
+        ctx.close()
+
+
+def test_microbench_mad_u64_is_a_hardware_ceiling():
+    """kzgx_microbench_mad_u64: lane-ops/s of v_mad_u64_u32 issue on the whole
+    GPU; profiles/r01_micro_valu.txt measured 3.19e13 (256 CUs, 2.4 GHz peak
+    clock: <= 256 x 4 SIMD x 16 lanes x 2.4e9 = 3.9e13)"""
+    import kzgx
+    import kzg_ref as K
+    ctx = kzgx.Context("BN254")
+    try:
+        ctx.gen_srs(K.default_tau(K.BN254), 8)
+        r = ctx.microbench_mad_u64()
+        assert 1.0e13 < r < 4.0e13, r
+    finally:
+        ctx.close()

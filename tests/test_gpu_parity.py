@@ -254,3 +254,58 @@ def test_large_single_msm_chunked(name, C, n, ctx_factory):
     sc[n // 2] = 0
     out, inf = ctx.msm(limbs(sc))
     assert pt(name, out, inf) == K.commit_via_tau(C, tau, sc)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_prove_range_duplicate_point_raises(name, C, ctx_factory, oracle_c):
+    """kzgx_prove_range with a repeated opening point: the reference's
+    interpolation (NTL polyfit) fails on it, so does the opening
+    (KZGX_ERR_DIV_ZERO), even though P div Z alone would be defined"""
+    import kzgx
+    ctx = ctx_factory(name)
+    ctx.load_srs(oracle_c.gen_srs(name, 5, 40))
+    with pytest.raises(kzgx.KzgxError) as e:
+        ctx.prove_range(limbs(list(range(1, 30))), limbs([3, 7, 3]))
+    assert e.value.status == -8  # KZGX_ERR_DIV_ZERO
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("npts", [2, 5])
+def test_prove_range_long_polynomial_few_points(name, C, npts, oracle_c):
+    """few points on a long polynomial: degree 2^16 opened at
+    2 / 5 points goes through the division chain (one chip-wide synthetic
+    division per point), not the quadratic Newton route; exact against the
+    known-tau identity, and bounded in time"""
+    import time
+    import kzgx
+    tau = K.default_tau(C)
+    n = (1 << 16) + 1
+    P = K.random_scalars(C, n, seed=0xD1 + npts)
+    xs = [3 + 17 * k for k in range(npts)]
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(tau, n)
+        ctx.prove_range(limbs(P[:1000]), limbs(xs))  # warm
+        t0 = time.perf_counter()
+        out, inf = ctx.prove_range(limbs(P), limbs(xs))
+        dt = time.perf_counter() - t0
+        # [q(tau)]G1 with q = P div Z: q(tau) = (P(tau) - I(tau)) / Z(tau)
+        r = C.r
+        ptau = K.poly_eval(C, P, tau)
+        Z = 1
+        for x in xs:
+            Z = Z * (tau - x) % r
+        # I(tau) by Lagrange over the points
+        I = 0
+        for i, xi in enumerate(xs):
+            num, den = 1, 1
+            for j, xj in enumerate(xs):
+                if j != i:
+                    num = num * (tau - xj) % r
+                    den = den * (xi - xj) % r
+            I = (I + K.poly_eval(C, P, xi) * num * pow(den, -1, r)) % r
+        qt = (ptau - I) * pow(Z, -1, r) % r
+        assert pt(name, out, inf) == K.scalar_mul(C, (C.gx, C.gy), qt)
+        assert dt < 2.0, dt
+    finally:
+        ctx.close()
