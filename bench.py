@@ -79,7 +79,8 @@ def parse():
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic; default cfg2 22: "
                          "2048 MSMs x 3 wavefronts = two full residencies per launch; cfg4 65: 2048 x 1 wavefront; "
                          "else 16)")
-    ap.add_argument("--table-gb", type=float, default=200.0, help="cfg5: fixed-base table budget per GPU (GB)")
+    ap.add_argument("--table-gb", type=float, default=0.0,
+                    help="cfg5: fixed-base table budget per GPU (GB; 0 = free HBM minus 8 GB)")
     ap.add_argument("--serial", action="store_true",
                     help="commit and proof batches on one stream (exact per-kernel event timing)")
     ap.add_argument("--split", type=int, default=1, help="sub-batches (each on its own stream) per batch")
@@ -730,12 +731,15 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx.set_segment(args.segment)
     ctx.gen_srs(tau, max(count, 1), start)
     # fixed-base table over this rank's shard: the widest window whose table
-    # fits the budget (2^20 points on 1 GPU: c = 7, 158.9 GB; 2^17 per GPU on
-    # 8 GPUs: c = 10, 139.6 GB).  Setup work, outside the timed region.
+    # fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB; 2^19 on 2:
+    # c = 9, 249.1 GB; 2^18 on 4: c = 10, 223.3 GB; 2^17 on 8: c = 11,
+    # 206.2 GB), stored point-major (msm_fixed.hip).  Setup work, outside the
+    # timed region.
     t_setup = time.perf_counter()
     fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
     if fixed_bits:
-        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1), budget=args.table_gb * 1e9)
+        fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1),
+                                             budget=args.table_gb * 1e9 if args.table_gb > 0 else None)
     t_setup = time.perf_counter() - t_setup
     rng = np.random.default_rng(0x4B5A47)  # same full polynomial on every rank
     coeffs_h = random_fr(rng, (n,), C.r)

@@ -237,10 +237,23 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
 }
 
 // the mixed addition every accumulation loop inlines: 0 = classic (one
-// product at a time), 1 = grouped independent products (nway)
-#ifndef KZGX_MADD_VARIANT
-#define KZGX_MADD_VARIANT 1
+// product at a time), 1 = grouped independent products (nway).  Per curve
+// (KZGX_MADD_VARIANT overrides both): chosen by the interleaved A/B of the
+// bench kernels in DESIGN.md section 3.
+#ifdef KZGX_MADD_VARIANT
+#define KZGX_MADD_VARIANT_BN KZGX_MADD_VARIANT
+#define KZGX_MADD_VARIANT_BLS KZGX_MADD_VARIANT
 #endif
+#ifndef KZGX_MADD_VARIANT_BN
+#define KZGX_MADD_VARIANT_BN 1
+#endif
+#ifndef KZGX_MADD_VARIANT_BLS
+#define KZGX_MADD_VARIANT_BLS 1
+#endif
+template <class C>
+constexpr int madd_variant() {
+  return C::Fp29::L <= 9 ? KZGX_MADD_VARIANT_BN : KZGX_MADD_VARIANT_BLS;
+}
 template <class C, int V>
 KZGX_DEV Xyzz<C> xyzz_add_affine_v(const Xyzz<C>& p, const Affine<C>& a) {
   if constexpr (V == 0) {
@@ -259,7 +272,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_v(const Xyzz<C>& p, const Affine<C>& a) {
 }
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_add_affine_impl(const Xyzz<C>& p, const Affine<C>& a) {
-  return xyzz_add_affine_v<C, KZGX_MADD_VARIANT>(p, a);
+  return xyzz_add_affine_v<C, madd_variant<C>()>(p, a);
 }
 
 // p + q (add-2008-s)

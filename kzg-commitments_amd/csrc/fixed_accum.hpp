@@ -33,6 +33,17 @@ constexpr int packed_words() {
   return fixed_l29<C>() ? affine_words<C>() : 2 * C::Fp::N;
 }
 
+// Where entry (i, w, j) of the table lives: word (i is + w ws + j PW).
+//  * window-major M[w][i][j] (is = H PW, ws = n_t H PW): a wavefront's lanes
+//    (consecutive points, one window) read within one window slice;
+//  * point-major M[i][w][j] (is = W H PW, ws = H PW): the W windows of a point
+//    are adjacent, so one thread's consecutive terms (k_fixed_accum_flat walks
+//    a point's windows in order) stay within W H PW words -- 148 KB at c = 7
+//    -- instead of jumping a whole window slice (4.3 GB at cfg5) per term.
+struct TabStrides {
+  size_t is, ws;  // words
+};
+
 template <class C, int CB>
 struct FixedWin {
   // signed digits of a scalar < r need W c >= bits(r) + 1: the top digit
@@ -191,7 +202,7 @@ struct FixedTerms {
   const uint32_t* sc;
   const uint8_t* inf;
   const uint32_t* tab;
-  size_t wstride;  // words between windows
+  TabStrides ts;
   uint32_t i, T;
   int w;
   uint32_t s[8], carry;
@@ -215,7 +226,7 @@ struct FixedTerms {
     }
     const int dd = next_digit<CB>(s, carry);
     d = skip ? 0 : dd;
-    const uint32_t* p = tab + (size_t)i * H * PW + (size_t)w * wstride + (size_t)((d < 0 ? -d : d) - (d != 0)) * PW;
+    const uint32_t* p = tab + (size_t)i * ts.is + (size_t)w * ts.ws + (size_t)((d < 0 ? -d : d) - (d != 0)) * PW;
     w++;
     return p;
   }
@@ -231,10 +242,10 @@ typedef __attribute__((address_space(3))) void* kzgx_lptr_t;
 // thread t of MSM b sums its terms (FixedTerms) into one XYZZ accumulator
 // with mixed additions (variant V, curve.hpp).  Software pipeline: the
 // table lookups of the next PF terms are in flight during each addition.
-template <class C, int CB, int V = KZGX_MADD_VARIANT, int PF = KZGX_FIXED_PF>
+template <class C, int CB, int V = madd_variant<C>(), int PF = KZGX_FIXED_PF>
 __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
     const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
-    uint32_t n_t, const uint8_t* __restrict__ inf, uint32_t T, uint32_t* __restrict__ part) {
+    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t T, uint32_t* __restrict__ part) {
   constexpr int XW = xyzz_words<C>();
   using G = FixedTerms<C, CB>;
   const uint32_t b = blockIdx.y;
@@ -256,7 +267,7 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
       g.sc = scalars + (size_t)b * stride_words;
       g.inf = inf;
       g.tab = tab;
-      g.wstride = (size_t)n_t * G::H * G::PW;
+      g.ts = ts;
       g.i = t;
       g.T = T;
       g.load();
@@ -288,7 +299,7 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
     g.sc = scalars + (size_t)b * stride_words;
     g.inf = inf;
     g.tab = tab;
-    g.wstride = (size_t)n_t * G::H * G::PW;
+    g.ts = ts;
     g.i = t;
     g.T = T;
     g.load();
@@ -299,8 +310,8 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
       dq[k] = 0;
       if (k < E) pq[k] = packed_fetch<C>(g.next(dq[k]));
     }
-#pragma unroll 1
-    for (int e = 0; e < E; e++) {
+    // one term: add the queued entry, queue the lookup PF terms ahead
+    auto step = [&](int e) {
       Affine<C> cur = packed_unpack<C>(pq[0]);
       const int d = dq[0];
 #pragma unroll
@@ -316,7 +327,12 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
         if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
         acc = xyzz_add_affine_v<C, V>(acc, cur);
       }
-    }
+    };
+    // (a two-term body, for the allocator to alternate the accumulator
+    // between two register sets instead of copying it back, spilled: 368 B
+    // of scratch on BN254, 704 B on BLS12-381)
+#pragma unroll 1
+    for (int e = 0; e < E; e++) step(e);
    }
   }
   xyzz_store<C>(part + ((size_t)b * T + t) * XW, acc);

@@ -9,6 +9,7 @@
 // does not depend on the scalars is paid once, at setup time:
 //
 //   M[w][i][j] = (j + 1) 2^(c w) P_i      w < W, i < n_t, j < H = 2^(c-1)
+// stored window-major, or point-major for small c (TabStrides, fixed_accum.hpp)
 //
 // stored affine, Montgomery form (64-B packed words on BN254, 112-B radix-2^29
 // limbs on BLS12-381, see fixed_l29).  A scalar s_i with signed c-bit digits
@@ -62,11 +63,12 @@ __global__ __launch_bounds__(64) void k_fixed_bases(const uint32_t* __restrict__
   }
 }
 
-// M[w][i][j0 + j] = (j0 + j + 1) B[w][i], j < J; thread per (w, i, block)
+// M(w, i, j0 + j) = (j0 + j + 1) B[w][i], j < J; thread per (w, i, block),
+// written at the table's strides (TabStrides)
 template <class C>
 __global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restrict__ bases,
                                                         const uint8_t* __restrict__ inf, uint32_t n, int W, uint32_t H,
-                                                        uint32_t J, uint64_t g0, uint64_t cnt,
+                                                        uint32_t J, uint64_t g0, uint64_t cnt, TabStrides ts,
                                                         uint32_t* __restrict__ tab) {
   constexpr int PW = packed_words<C>();
   const uint64_t gl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -76,7 +78,8 @@ __global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restri
   const uint32_t blk = (uint32_t)(g % nblk);
   const uint64_t wi = g / nblk;  // w * n + i
   const uint32_t i = (uint32_t)(wi % n);
-  uint32_t* out = tab + (wi * H + (uint64_t)blk * J) * PW;
+  const uint32_t w = (uint32_t)(wi / n);
+  uint32_t* out = tab + (uint64_t)i * ts.is + (uint64_t)w * ts.ws + (uint64_t)blk * J * PW;
   if (inf[i]) {  // never read: the MSM skips infinite SRS points
     for (uint32_t j = 0; j < J * PW; j++) out[j] = 0;
     return;
@@ -172,7 +175,7 @@ KZGX_DEV Xyzz<C> xyzz_shfl_xor_add(const Xyzz<C>& acc, int off) {
 template <class C, int CB>
 __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restrict__ scalars, uint32_t n,
                                                         uint32_t n_pad, size_t stride_words,
-                                                        const uint32_t* __restrict__ tab, uint32_t n_t,
+                                                        const uint32_t* __restrict__ tab, TabStrides ts,
                                                         const uint8_t* __restrict__ inf, int WG, uint32_t Q,
                                                         uint32_t* __restrict__ part) {
   constexpr int PW = packed_words<C>();
@@ -194,15 +197,14 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
       s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
     }
     scalar_reduce<C>(s);
-    const uint32_t* base = tab + (size_t)i * H * PW;
-    const size_t wstride = (size_t)n_t * H * PW;
+    const uint32_t* base = tab + (size_t)i * ts.is;
     uint32_t carry = 0;
 #pragma unroll 1
     for (int w = 0; w < w1; w++) {
       const int d = next_digit<CB>(s, carry);  // windows below w0 only carry
       if (w < w0 || d == 0) continue;
       Affine<C> cur =
-          packed_unpack<C>(packed_fetch<C>(base + (size_t)w * wstride + (size_t)((d < 0 ? -d : d) - 1) * PW));
+          packed_unpack<C>(packed_fetch<C>(base + (size_t)w * ts.ws + (size_t)((d < 0 ? -d : d) - 1) * PW));
       if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
       acc = xyzz_add_affine_impl<C>(acc, cur);
     }
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(64) void k_fixed_fold_finish(const uint32_t* __rest
 template <class C, int CB>
 __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat(
     const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
-    uint32_t n_t, const uint8_t* __restrict__ inf, uint32_t Q, uint32_t T, uint32_t* __restrict__ part) {
+    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t Q, uint32_t T, uint32_t* __restrict__ part) {
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
@@ -260,7 +262,6 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
   const uint32_t b = blockIdx.y;
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;  // < T: the grid is exact
   const uint32_t* sc = scalars + (size_t)b * stride_words;
-  const size_t wstride = (size_t)n_t * H * PW;  // words between windows
   const size_t e_end = (size_t)n * W;
   size_t e = (size_t)t * Q;
   const size_t e1 = e + Q < e_end ? e + Q : e_end;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
     for (int k = 0; k < w; k++) (void)next_digit<CB>(s, carry);  // carry of the lower windows
     // the digit of the current term and its table entry's address
     auto fetch = [&](int dd) {
-      return packed_fetch<C>(tab + (size_t)i * H * PW + (size_t)w * wstride +
+      return packed_fetch<C>(tab + (size_t)i * ts.is + (size_t)w * ts.ws +
                              (size_t)((dd < 0 ? -dd : dd) - (dd != 0)) * PW);
     };
     auto advance = [&]() {
@@ -334,6 +335,30 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
 // --------------------------------------------------------------------------
 constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
 
+// Table layout (TabStrides): point-major for c <= KZGX_FIXED_PM_MAX_C (the
+// few-large-MSM tables, walked point by point by k_fixed_accum_flat),
+// window-major above.  KZGX_FIXED_POINT_MAJOR=0/1 forces one (A/B).
+#ifndef KZGX_FIXED_PM_MAX_C
+#define KZGX_FIXED_PM_MAX_C 12
+#endif
+static bool fixed_point_major(int c) {
+  static const char* e = std::getenv("KZGX_FIXED_POINT_MAJOR");
+  if (e && *e) return std::atoi(e) != 0;
+  return c <= KZGX_FIXED_PM_MAX_C;
+}
+
+template <class C>
+static TabStrides fixed_strides(bool point_major, int W, size_t n, uint64_t H) {
+  constexpr size_t PW = packed_words<C>();
+  if (point_major) return TabStrides{(size_t)W * H * PW, H * PW};
+  return TabStrides{H * PW, n * H * PW};
+}
+
+template <class C>
+static TabStrides tab_strides(const FixedTable& ft) {
+  return fixed_strides<C>(ft.point_major, ft.W, ft.n_t, 1ull << (ft.c - 1));
+}
+
 template <class C>
 static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   FixedTable& ft = ctx->fixed;
@@ -373,6 +398,8 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
                      d_bases, d_inf);
   const uint32_t J = (uint32_t)(H < FIXED_J ? H : FIXED_J);
   const uint64_t tasks = (uint64_t)W * n * (H / J);
+  ft.point_major = fixed_point_major(c);
+  const TabStrides ts = fixed_strides<C>(ft.point_major, W, n, H);
   // bounded launches of <= 2^22 threads each, synchronised per slice so one
   // setup never queues seconds of work behind a single dispatch
   const uint64_t slice = 1ull << 22;
@@ -381,7 +408,7 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
     {
       ProfScope p(ctx, st, "fixed_build");
       hipLaunchKernelGGL(k_fixed_multiples<C>, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, d_bases, d_inf,
-                         (uint32_t)n, W, (uint32_t)H, J, s0, cnt, ft.d);
+                         (uint32_t)n, W, (uint32_t)H, J, s0, cnt, ts, ft.d);
     }
     KZGX_TRY_HIP(hipGetLastError());
     KZGX_TRY_HIP(hipStreamSynchronize(st));
@@ -433,7 +460,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
     KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
-                       (uint32_t)n_pad, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, WG, Q, wsp->fpart);
+                       (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), ft.inf, WG, Q, wsp->fpart);
     hipLaunchKernelGGL(k_fixed_fold_finish<C>, dim3((unsigned)batch), dim3(64), 0, st, wsp->fpart, Q, d_out,
                        d_out_inf);
     KZGX_TRY_HIP(hipGetLastError());
@@ -466,7 +493,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
       {
         ProfScope p(ctx, st, "msm_accum");
         hipLaunchKernelGGL((k_fixed_accum_flat<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                           (uint32_t)n, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, Q, T, ws.fpart);
+                           (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), ft.inf, Q, T, ws.fpart);
       }
       ProfScope p(ctx, st, "msm_reduce");
       // T / 64 wavefront partials per MSM: one more 64:1 level, then one
@@ -501,7 +528,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   {
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                       (uint32_t)n, stride_words, ft.d, (uint32_t)ft.n_t, ft.inf, T, ws.fpart);
+                       (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), ft.inf, T, ws.fpart);
   }
   if (wave_red) {
     ProfScope p(ctx, st, "msm_reduce");

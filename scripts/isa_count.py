@@ -15,7 +15,9 @@ not-taken edges to the back edge.  --per N divides the totals by N (e.g. the
 number of mixed additions per iteration).
 
 Used for bench.py's secondary.mad_issue (v_mad_u64_u32 per mixed addition)
-and DESIGN.md section 7.
+and DESIGN.md section 7:
+
+    python3 scripts/isa_count.py --profile profiles/r03_isa_counts.json
 """
 from __future__ import annotations
 
@@ -78,6 +80,35 @@ def hot_loop(body):
     return best[1], best[2]
 
 
+def common_path(body, lo, hi):
+    """the per-term common path: the accumulation loops compute the mixed
+    addition's products, then test (one limb first) whether the rare case
+    (the table point equals the accumulator: doubling) needs a full check;
+    `s_cbranch_execz <loop label>` skips that check and the doubling when no
+    lane needs it.  The common path is the loop from its first line to the
+    first conditional back edge after a basic block of >= 100
+    v_mad_u64_u32 (the products)"""
+    labels = {}
+    for i in range(lo, hi + 1):
+        m = LABEL.match(body[i])
+        if m:
+            labels[m.group(1)] = i
+    block_mads = 0
+    seen_products = False
+    for i in range(lo, hi + 1):
+        ln = body[i]
+        if LABEL.match(ln) or BRANCH.match(ln):
+            seen_products = seen_products or block_mads >= 100
+            block_mads = 0
+        elif "v_mad_u64_u32" in ln:
+            block_mads += 1
+        m = BRANCH.match(ln)
+        if (seen_products and m and m.group(1) != "s_branch" and m.group(2) in labels
+                and labels[m.group(2)] < i):
+            return body[lo:i + 1]
+    return body[lo:hi + 1]
+
+
 def fallthrough_path(body, lo, hi):
     """instructions on the not-taken path of every forward conditional branch
     from the loop head to the back edge (unconditional forward jumps are
@@ -116,7 +147,46 @@ def summarize(h, per):
     return res
 
 
+KERNELS = {  # bench.py's secondary.mad_issue key -> k_fixed_accum instantiation
+    "BN254_c16": "k_fixed_accumINS_7BN254G1ELi16E",
+    "BN254_c17": "k_fixed_accumINS_7BN254G1ELi17E",
+    "BLS12381_c16": "k_fixed_accumINS_10BLS12381G1ELi16E",
+    "BLS12381_c17": "k_fixed_accumINS_10BLS12381G1ELi17E",
+}
+
+
+def emit_profile(out_path):
+    """compile csrc/msm_fixed.hip to gfx950 assembly and write the per-term
+    common-path counts of the table kernels (one mixed addition per term)"""
+    import os
+    import subprocess
+    import tempfile
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    src = os.path.join(root, "kzg-commitments_amd", "csrc", "msm_fixed.hip")
+    with tempfile.TemporaryDirectory() as tmp:
+        asm = os.path.join(tmp, "msm_fixed.s")
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
+                        "-S", "-o", asm, src], check=True, capture_output=True)
+        with open(asm) as f:
+            lines = f.read().splitlines()
+    res = {"generated_by": "python3 scripts/isa_count.py --profile " + os.path.relpath(out_path, root),
+           "unit": "instructions per table term (one XYZZ mixed addition plus the term's fetch/unpack/digit "
+                   "work) on the loop's common path: from the loop head to the first conditional back edge "
+                   "after the products (the rare full equality check and doubling are skipped there)"}
+    for key, needle in KERNELS.items():
+        body = kernel_body(lines, needle)
+        lo, hi = hot_loop(body)
+        c = summarize(histogram(common_path(body, lo, hi)), 1.0)
+        res[key] = {"v_mad_u64_u32": c["v_mad_u64_u32"], "valu": c["valu"], "salu": c["salu"],
+                    "s_nop": c["top"].get("s_nop", 0), "non_mad_valu": c["valu"] - c["v_mad_u64_u32"]}
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--profile":
+        return emit_profile(sys.argv[2])
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
     ap.add_argument("kernel")
@@ -129,12 +199,13 @@ def main():
     lo, hi = hot_loop(body)
     loop = body[lo:hi + 1]
     path = fallthrough_path(body, lo, hi)
+    common = common_path(body, lo, hi)
     out = {"kernel": a.kernel, "loop_lines": hi - lo, "loop": summarize(histogram(loop), a.per),
-           "path": summarize(histogram(path), a.per)}
+           "path": summarize(histogram(path), a.per), "common": summarize(histogram(common), a.per)}
     if a.json:
         print(json.dumps(out))
     else:
-        for k in ("loop", "path"):
+        for k in ("loop", "path", "common"):
             s = out[k]
             print("%s: v_mad_u64_u32 %.0f  VALU %.0f  SALU %.0f" % (k, s["v_mad_u64_u32"], s["valu"], s["salu"]))
             print("   ", ", ".join("%s %.0f" % kv for kv in s["top"].items()))

@@ -112,19 +112,21 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  // window-major layout (msm_fixed.hip, TabStrides)
+  const TabStrides ts{(size_t)FixedWin<C, CB>::H * PW, (size_t)n * FixedWin<C, CB>::H * PW};
   double ms[3];
   for (int v = 0; v < 3; v++) {
     for (int rep = 0; rep < 3; rep++) {
       hipEventRecord(e0, 0);
       if (v == 0)
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           n, d_inf, T, d_p0);
+                           ts, d_inf, T, d_p0);
       else if (v == 1)
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 1, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           n, d_inf, T, d_p1);
+                           ts, d_inf, T, d_p1);
       else  // loads and digit recoding only: the memory path's own rate
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 2, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           n, d_inf, T, d_p0 + 0 * pw);
+                           ts, d_inf, T, d_p0 + 0 * pw);
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float m = 0;
@@ -133,7 +135,7 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
     }
   }
   // rerun classic into d_p0 (the probe overwrote it)
-  hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab, n,
+  hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab, ts,
                      d_inf, T, d_p0);
   std::vector<uint32_t> h0(pw), h1(pw);
   hipMemcpy(h0.data(), d_p0, pw * 4, hipMemcpyDeviceToHost);
