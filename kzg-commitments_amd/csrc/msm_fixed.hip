@@ -181,7 +181,6 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
-  constexpr uint32_t H = FixedWin<C, CB>::H;
   const uint32_t b = blockIdx.y;
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;  // < G n_pad: grid is exact
   const uint32_t g = t / n_pad, i = t - g * n_pad;
@@ -258,7 +257,6 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
-  constexpr uint32_t H = FixedWin<C, CB>::H;
   const uint32_t b = blockIdx.y;
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;  // < T: the grid is exact
   const uint32_t* sc = scalars + (size_t)b * stride_words;
