@@ -95,6 +95,14 @@ int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
  * c in {4, 7..17}; BN254 c = 17 over 4097 points (15 windows) takes
  * 257.8 GB of device memory, c = 16 137.5 GB. */
 int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
+/* table layout for the next build: -1 = automatic (the default: point-major
+ * M[i][w][j] for c <= 12, where the few-large-MSM kernel walks one point's
+ * windows in order; window-major M[w][i][j] above), 0 = window-major,
+ * 1 = point-major.  Results are identical; only speed differs (DESIGN.md
+ * section 3).  Extension with no reference counterpart. */
+int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout);
+/* layout of the built table: *point_major = 1 (M[i][w][j]) or 0 (M[w][i][j]) */
+int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major);
 /* built table: window bits (0 = none), points covered, device bytes */
 int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
 /* device bytes a table of window c over n_points would take (no context) */

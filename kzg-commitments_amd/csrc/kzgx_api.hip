@@ -237,6 +237,19 @@ int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points) {
   return KZGX_OK;
 }
 
+int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout) {
+  KZGX_TRY(activate(ctx));
+  if (layout < -1 || layout > 1) return KZGX_ERR_ARG;
+  ctx->c.fixed.layout_req = layout;
+  return KZGX_OK;
+}
+
+int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major) {
+  if (!ctx || !point_major) return KZGX_ERR_ARG;
+  *point_major = ctx->c.fixed.point_major ? 1 : 0;
+  return KZGX_OK;
+}
+
 int kzgx_fixed_base_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes) {
   if (!ctx) return KZGX_ERR_ARG;
   if (c) *c = ctx->c.fixed.c;

@@ -58,7 +58,8 @@ struct FixedTable {
   uint32_t pts_per_thread = 0;  // 0 = automatic (fixed_msm_impl)
   int c = 0, W = 0;     // built table
   size_t n_t = 0;
-  bool point_major = false;  // M[i][w][j] instead of M[w][i][j] (msm_fixed.hip)
+  int layout_req = -1;       // -1 automatic, 0 window-major, 1 point-major
+  bool point_major = false;  // built: M[i][w][j] instead of M[w][i][j] (msm_fixed.hip)
   uint32_t* d = nullptr;
   size_t bytes = 0;
   uint8_t* inf = nullptr;  // [n_t] infinite SRS points (skipped)

@@ -335,13 +335,16 @@ constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
 
 // Table layout (TabStrides): point-major for c <= KZGX_FIXED_PM_MAX_C (the
 // few-large-MSM tables, walked point by point by k_fixed_accum_flat),
-// window-major above.  KZGX_FIXED_POINT_MAJOR=0/1 forces one (A/B).
+// window-major above (profiles/r03_cfg5_table_layout.json,
+// r03_ab_point_major_cfg2.json).  kzgx_set_fixed_base_layout or
+// KZGX_FIXED_POINT_MAJOR=0/1 force one.
 #ifndef KZGX_FIXED_PM_MAX_C
 #define KZGX_FIXED_PM_MAX_C 12
 #endif
-static bool fixed_point_major(int c) {
+static bool fixed_point_major(int c, int layout_req) {
   static const char* e = std::getenv("KZGX_FIXED_POINT_MAJOR");
   if (e && *e) return std::atoi(e) != 0;
+  if (layout_req >= 0) return layout_req != 0;
   return c <= KZGX_FIXED_PM_MAX_C;
 }
 
@@ -396,7 +399,7 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
                      d_bases, d_inf);
   const uint32_t J = (uint32_t)(H < FIXED_J ? H : FIXED_J);
   const uint64_t tasks = (uint64_t)W * n * (H / J);
-  ft.point_major = fixed_point_major(c);
+  ft.point_major = fixed_point_major(c, ft.layout_req);
   const TabStrides ts = fixed_strides<C>(ft.point_major, W, n, H);
   // bounded launches of <= 2^22 threads each, synchronised per slice so one
   // setup never queues seconds of work behind a single dispatch

@@ -23,6 +23,7 @@ EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
+    "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout",
     "kzgx_microbench_mad_u64", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
@@ -79,6 +80,8 @@ def lib():
             "kzgx_fixed_base_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
             "kzgx_fixed_base_bytes": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, sz, ctypes.POINTER(sz)]),
             "kzgx_set_fixed_base_budget": (ctypes.c_int, [vp, sz, sz, intp]),
+            "kzgx_set_fixed_base_layout": (ctypes.c_int, [vp, ctypes.c_int]),
+            "kzgx_fixed_base_layout": (ctypes.c_int, [vp, intp]),
             "kzgx_microbench_mad_u64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_microbench_mixed_add": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
@@ -201,6 +204,15 @@ class Context:
         """Precompute the signed-digit multiples table for the first n_points
         SRS points (c = 0: off).  Built now if an SRS is installed."""
         _chk(lib().kzgx_set_fixed_base(self.h, c, n_points), "kzgx_set_fixed_base")
+
+    def set_fixed_base_layout(self, layout: int):
+        """-1 automatic, 0 window-major, 1 point-major (next table build)"""
+        _chk(lib().kzgx_set_fixed_base_layout(self.h, layout), "kzgx_set_fixed_base_layout")
+
+    def fixed_base_point_major(self) -> bool:
+        pm = ctypes.c_int(0)
+        _chk(lib().kzgx_fixed_base_layout(self.h, ctypes.byref(pm)), "kzgx_fixed_base_layout")
+        return bool(pm.value)
 
     def fixed_base_info(self):
         c = ctypes.c_int(0)

@@ -222,6 +222,40 @@ def test_fixed_flat_terms(name, C, tau_kind, batch, fresh_ctx):
         assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
 
 
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("c", [7, 8, 12, 13])
+def test_fixed_table_layouts_agree(name, C, c, fresh_ctx, oracle_c):
+    """Window-major M[w][i][j] and point-major M[i][w][j] tables
+    (kzgx_set_fixed_base_layout; automatic = point-major for c <= 12) give
+    the oracle's sums on every kernel that reads them: the latency kernel
+    (one small MSM), the batched kernel (a batch of 20) and the flattened-term
+    kernel (one MSM with >= 8 terms per resident lane)."""
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C)
+    n_small, n_big = 300, 50001 if c <= 8 else 4097
+    ctx.gen_srs(tau, n_big)
+    sc = K.random_scalars(C, n_big, seed=1300 + c)
+    sc[1], sc[2] = 0, C.r - 1
+    S = limbs(sc)
+    polys = [K.random_scalars(C, n_small, seed=1400 + b) for b in range(20)]
+    SB = np.concatenate([limbs(P) for P in polys])
+    exp_small = oracle_c.msm_naive(name, oracle_c.gen_srs(name, tau, n_small), S[:n_small])
+    exp_big = K.commit_via_tau(C, tau, sc)
+    for layout, want_pm in ((-1, c <= 12), (0, False), (1, True)):
+        ctx.set_fixed_base_layout(layout)
+        ctx.set_fixed_base(c, n_big)
+        assert ctx.fixed_base_point_major() == want_pm, layout
+        out, inf = ctx.msm(S[:n_small])
+        assert pt(name, out, inf) == exp_small, (layout, "latency")
+        out, inf = ctx.msm_batch(SB, n_small, 20)
+        for b in (0, 7, 19):
+            assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), (layout, "batch", b)
+        out, inf = ctx.msm(S)
+        assert pt(name, out, inf) == exp_big, (layout, "large")
+    with pytest.raises(Exception):
+        ctx.set_fixed_base_layout(2)
+
+
 def test_fixed_base_budget_picks_the_widest_fitting_window():
     """kzgx_set_fixed_base_budget: the widest c whose table fits the budget
     (kzgx_fixed_base_bytes), none below c = 7 (Pippenger stays); exact MSMs
