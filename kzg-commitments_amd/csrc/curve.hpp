@@ -202,6 +202,25 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
   if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
 #endif
   F29<F> U2, S2;
+#ifdef KZGX_NWAY_TRI
+  // (U2, S2), (P^2, R^2), (PPP, Q, ZZ3) three in lockstep, (Y3, ZZZ3) with
+  // Y3's two products and ZZZ3's as three chains (field29.hpp "three chains")
+  f29_mul_x2<F>(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
+  const F29<F> P = f29_sub<F>(U2, p.X, F::P8);  // < 10m
+  const F29<F> R = f29_sub<F>(S2, p.Y, F::P4);  // < 6m
+  F29<F> PP, RR;
+  f29_sqr_x2<F>(P, R, PP, RR);                   // < 2m each
+  if (f29_is_zero_lt2m<F>(PP)) {
+    if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);
+    return xyzz_inf<C>();
+  }
+  F29<F> PPP, Q;
+  Xyzz<C> r;
+  f29_mul_x3<F>(P, PP, p.X, PP, p.ZZ, PP, PPP, Q, r.ZZ);
+  r.X = f29_sub<F>(RR, f29_add_2x_lazy<F>(PPP, Q), F::P6);  // < 8m
+  f29_mul2_mul<F>(R, f29_sub<F>(Q, r.X, F::P8), KZGX_NEG_Y1(p.Y), PPP, p.ZZZ, PPP, r.Y, r.ZZZ);
+  return r;
+#else
 #if KZGX_NWAY_PAIRS
   f29_mul_x2<F>(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
 #else
@@ -234,6 +253,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
   r.ZZZ = f29_mul_chain<F>(p.ZZZ, PPP);
 #endif
   return r;
+#endif
 }
 
 // the mixed addition every accumulation loop inlines: 0 = classic (one

@@ -297,12 +297,183 @@ struct PLimbs {
   }
 };
 
+// ---- Paired chains (KZGX_MAD_PAIR) ----
+// The scheduler runs each of two independent column chains for several
+// columns before it switches to the other, so consecutive mads read each
+// other's result: every one waits out the mad's latency and carries the
+// `s_nop 0` that gfx950's hazard rule puts between two dependent 64-bit VALU
+// results (hipcc -S).  Here one asm statement advances both chains by one mad,
+// so the two mads of a step are independent and the next step's first mad
+// is one instruction behind its producer (the one wait state the rule asks).
+// The unused carry-out goes to a scratch SGPR pair.
+KZGX_DEV void mad_pair(uint64_t& a0, uint32_t x0, uint32_t y0, uint64_t& a1, uint32_t x1, uint32_t y1) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_mad_u64_u32 %1, %2, %5, %6, %1"
+      : "+v"(a0), "+v"(a1), "=&s"(cc)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+}
+
+// column K of a0 b0 and of a1 b1, in lockstep
+template <class F, int K>
+KZGX_DEV void mc_prod2(MontChain<F>& c0, const F29<F>& a0, const F29<F>& b0, MontChain<F>& c1, const F29<F>& a1,
+                       const F29<F>& b1) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int j = K - i;
+    if (j >= 0 && j < F::L) mad_pair(c0.acc, a0.v[i], b0.v[j], c1.acc, a1.v[i], b1.v[j]);
+  }
+}
+
+// column K of a0^2 and of a1^2 (dd = 2a limb-wise), in lockstep
+template <class F, int K>
+KZGX_DEV void mc_sqr2(MontChain<F>& c0, const F29<F>& a0, const F29<F>& dd0, MontChain<F>& c1, const F29<F>& a1,
+                      const F29<F>& dd1) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int j = K - i;
+    if (j > i && j < F::L) mad_pair(c0.acc, a0.v[i], dd0.v[j], c1.acc, a1.v[i], dd1.v[j]);
+  }
+  if constexpr ((K & 1) == 0 && (K >> 1) < F::L)
+    mad_pair(c0.acc, a0.v[K >> 1], a0.v[K >> 1], c1.acc, a1.v[K >> 1], a1.v[K >> 1]);
+}
+
+// mc_reduce of two chains in lockstep
+template <class F, int K>
+KZGX_DEV void mc_reduce2(MontChain<F>& c0, F29<F>& r0, MontChain<F>& c1, F29<F>& r1, const uint32_t (&pl)[F::L]) {
+  constexpr int L = F::L;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    const int j = K - i;
+    if (i < K && j >= 1 && j < L) mad_pair(c0.acc, c0.q[i], pl[j], c1.acc, c1.q[i], pl[j]);
+  }
+  if constexpr (K < L) {
+    c0.q[K] = ((uint32_t)c0.acc * F::INV) & M29;
+    c1.q[K] = ((uint32_t)c1.acc * F::INV) & M29;
+    mad_pair(c0.acc, c0.q[K], pl[0], c1.acc, c1.q[K], pl[0]);
+  } else {
+    r0.v[K - L] = (uint32_t)c0.acc & M29;
+    r1.v[K - L] = (uint32_t)c1.acc & M29;
+  }
+  c0.acc >>= 29;
+  c1.acc >>= 29;
+  if constexpr (K == 2 * L - 2) {
+    r0.v[L - 1] = (uint32_t)c0.acc;
+    r1.v[L - 1] = (uint32_t)c1.acc;
+  }
+}
+
+// ---- Three chains in lockstep ----
+// gfx950 wants two wait states between a v_mad_u64_u32 and a VALU that reads
+// its result (hipcc -S: an `s_nop 0` wherever only one instruction separates
+// them, so two chains in lockstep still pay one pad per pair of mads).  With
+// three independent chains advanced round-robin every mad is two instructions
+// behind its producer: no pad at all.  Each pad costs about a quarter of a mad
+// issue at three waves per SIMD (scripts/micro_chain.hip,
+// profiles/r03_micro_chain.txt).
+KZGX_DEV void mad_tri(uint64_t& a0, uint32_t x0, uint32_t y0, uint64_t& a1, uint32_t x1, uint32_t y1, uint64_t& a2,
+                      uint32_t x2, uint32_t y2) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %3, %4, %5, %0\n\tv_mad_u64_u32 %1, %3, %6, %7, %1\n\tv_mad_u64_u32 %2, %3, %8, %9, %2"
+      : "+v"(a0), "+v"(a1), "+v"(a2), "=&s"(cc)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2));
+}
+// the same, the third chain starting from zero (a fresh column of a split
+// accumulator: src2 is the inline constant 0, no register to clear)
+KZGX_DEV void mad_tri_z(uint64_t& a0, uint32_t x0, uint32_t y0, uint64_t& a1, uint32_t x1, uint32_t y1, uint64_t& a2,
+                        uint32_t x2, uint32_t y2) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %3, %4, %5, %0\n\tv_mad_u64_u32 %1, %3, %6, %7, %1\n\tv_mad_u64_u32 %2, %3, %8, %9, 0"
+      : "+v"(a0), "+v"(a1), "=&v"(a2), "=&s"(cc)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2));
+}
+
+// column K of three products, in lockstep
+template <class F, int K>
+KZGX_DEV void mc_prod3(MontChain<F>& c0, const F29<F>& a0, const F29<F>& b0, MontChain<F>& c1, const F29<F>& a1,
+                       const F29<F>& b1, MontChain<F>& c2, const F29<F>& a2, const F29<F>& b2) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    const int j = K - i;
+    if (j >= 0 && j < F::L) mad_tri(c0.acc, a0.v[i], b0.v[j], c1.acc, a1.v[i], b1.v[j], c2.acc, a2.v[i], b2.v[j]);
+  }
+}
+
+// mc_reduce of three chains in lockstep
+template <class F, int K>
+KZGX_DEV void mc_reduce3(MontChain<F>& c0, F29<F>& r0, MontChain<F>& c1, F29<F>& r1, MontChain<F>& c2, F29<F>& r2,
+                         const uint32_t (&pl)[F::L]) {
+  constexpr int L = F::L;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    const int j = K - i;
+    if (i < K && j >= 1 && j < L) mad_tri(c0.acc, c0.q[i], pl[j], c1.acc, c1.q[i], pl[j], c2.acc, c2.q[i], pl[j]);
+  }
+  if constexpr (K < L) {
+    c0.q[K] = ((uint32_t)c0.acc * F::INV) & M29;
+    c1.q[K] = ((uint32_t)c1.acc * F::INV) & M29;
+    c2.q[K] = ((uint32_t)c2.acc * F::INV) & M29;
+    mad_tri(c0.acc, c0.q[K], pl[0], c1.acc, c1.q[K], pl[0], c2.acc, c2.q[K], pl[0]);
+  } else {
+    r0.v[K - L] = (uint32_t)c0.acc & M29;
+    r1.v[K - L] = (uint32_t)c1.acc & M29;
+    r2.v[K - L] = (uint32_t)c2.acc & M29;
+  }
+  c0.acc >>= 29;
+  c1.acc >>= 29;
+  c2.acc >>= 29;
+  if constexpr (K == 2 * L - 2) {
+    r0.v[L - 1] = (uint32_t)c0.acc;
+    r1.v[L - 1] = (uint32_t)c1.acc;
+    r2.v[L - 1] = (uint32_t)c2.acc;
+  }
+}
+
+// r0 = a0 b0 / R, r1 = a1 b1 / R, r2 = a2 b2 / R: three chains in lockstep
+template <class F>
+KZGX_DEV void f29_mul_x3(const F29<F>& a0, const F29<F>& b0, const F29<F>& a1, const F29<F>& b1, const F29<F>& a2,
+                         const F29<F>& b2, F29<F>& r0, F29<F>& r1, F29<F>& r2) {
+  const PLimbs<F> pl;
+  MontChain<F> c0, c1, c2;
+  c0.acc = c1.acc = c2.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_prod3<F, k>(c0, a0, b0, c1, a1, b1, c2, a2, b2);
+    mc_reduce3<F, k>(c0, r0, c1, r1, c2, r2, pl.v);
+  });
+}
+
+// r0 = (a b + c d) / R with one reduction, r1 = e f / R.  The products run as
+// three chains in lockstep (c d into a second accumulator of r0 that starts
+// from zero every column and is merged before the column's reduction), the
+// reductions as a pair.  Same bounds as f29_mul2 / f29_mul.
+template <class F>
+KZGX_DEV void f29_mul2_mul(const F29<F>& a, const F29<F>& b, const F29<F>& c, const F29<F>& d, const F29<F>& e,
+                           const F29<F>& f, F29<F>& r0, F29<F>& r1) {
+  const PLimbs<F> pl;
+  MontChain<F> c0, c1;
+  c0.acc = c1.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    constexpr int i0 = K < F::L ? 0 : K - F::L + 1;  // first term of column K
+    uint64_t side;
+    mad_tri_z(c0.acc, a.v[i0], b.v[K - i0], c1.acc, e.v[i0], f.v[K - i0], side, c.v[i0], d.v[K - i0]);
+#pragma unroll
+    for (int i = i0 + 1; i < F::L; i++) {
+      const int j = K - i;
+      if (j >= 0) mad_tri(c0.acc, a.v[i], b.v[j], c1.acc, e.v[i], f.v[j], side, c.v[i], d.v[j]);
+    }
+    c0.acc += side;
+    mc_reduce2<F, K>(c0, r0, c1, r1, pl.v);
+  });
+}
+
 // Independent Montgomery products computed side by side, every column of
 // every product ONE dependent v_mad_u64_u32 chain that starts from the
 // previous column's carry: a shift per column and no merge of two partial
 // chains (the compiler splits a lone product's columns into two chains for
 // latency and pays a 64-bit add per column to join them).  The chains of the
-// different products are independent, so the scheduler interleaves them.
+// different products are independent: with KZGX_MAD_PAIR they advance in
+// lockstep (mad_pair), otherwise the scheduler interleaves them.
 // Same output bounds as f29_mul / f29_sqr / f29_mul2.
 template <class F>
 KZGX_DEV void f29_mul_x2(const F29<F>& a0, const F29<F>& b0, const F29<F>& a1, const F29<F>& b1, F29<F>& r0,
@@ -312,10 +483,15 @@ KZGX_DEV void f29_mul_x2(const F29<F>& a0, const F29<F>& b0, const F29<F>& a1, c
   c0.acc = c1.acc = 0;
   static_for<0, 2 * F::L - 1>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
+#ifdef KZGX_MAD_PAIR
+    mc_prod2<F, k>(c0, a0, b0, c1, a1, b1);
+    mc_reduce2<F, k>(c0, r0, c1, r1, pl.v);
+#else
     mc_prod<F, k>(c0, a0, b0);
     mc_prod<F, k>(c1, a1, b1);
     mc_reduce<F, k>(c0, r0, pl.v);
     mc_reduce<F, k>(c1, r1, pl.v);
+#endif
   });
 }
 
@@ -332,10 +508,15 @@ KZGX_DEV void f29_sqr_x2(const F29<F>& a0, const F29<F>& a1, F29<F>& r0, F29<F>&
   c0.acc = c1.acc = 0;
   static_for<0, 2 * F::L - 1>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
+#ifdef KZGX_MAD_PAIR
+    mc_sqr2<F, k>(c0, a0, d0, c1, a1, d1);
+    mc_reduce2<F, k>(c0, r0, c1, r1, pl.v);
+#else
     mc_sqr<F, k>(c0, a0, d0);
     mc_sqr<F, k>(c1, a1, d1);
     mc_reduce<F, k>(c0, r0, pl.v);
     mc_reduce<F, k>(c1, r1, pl.v);
+#endif
   });
 }
 

@@ -189,11 +189,22 @@ constexpr int fixed_accum_waves() {
   return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : KZGX_FIXED_WAVES_BLS;
 }
 
+typedef __attribute__((address_space(1))) const void* kzgx_gptr_t;
+typedef __attribute__((address_space(3))) void* kzgx_lptr_t;
+
+KZGX_DEV void scalar_load(const uint32_t* __restrict__ src, uint32_t (&s)[8]) {
+  const uint4 lo = reinterpret_cast<const uint4*>(src)[0];
+  const uint4 hi = reinterpret_cast<const uint4*>(src)[1];
+  s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
+  s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+}
+
 // The digit terms of one accumulation thread, in order: points i = t,
 // t + T, t + 2T, ... (a wavefront reads 64 consecutive scalars per point
 // step), windows w = 0 .. W - 1 of each.  next() recodes the next signed
 // digit (0: no addition; every term of an infinite SRS point is 0) and
-// returns its table entry.
+// returns its table entry.  inf may be null: no SRS point is infinite (the
+// table build checks), and no flag is read.
 template <class C, int CB>
 struct FixedTerms {
   static constexpr int PW = packed_words<C>();
@@ -209,13 +220,10 @@ struct FixedTerms {
   bool skip;
 
   KZGX_DEV void load() {
-    const uint4 lo = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[0];
-    const uint4 hi = reinterpret_cast<const uint4*>(sc + (size_t)i * 8)[1];
-    s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
-    s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+    scalar_load(sc + (size_t)i * 8, s);
     scalar_reduce<C>(s);
     carry = 0;
-    skip = inf[i] != 0;
+    skip = inf != nullptr && inf[i] != 0;
     w = 0;
   }
   // only while terms remain
@@ -235,9 +243,6 @@ struct FixedTerms {
 #ifndef KZGX_FIXED_PF
 #define KZGX_FIXED_PF 1
 #endif
-
-typedef __attribute__((address_space(1))) const void* kzgx_gptr_t;
-typedef __attribute__((address_space(3))) void* kzgx_lptr_t;
 
 // thread t of MSM b sums its terms (FixedTerms) into one XYZZ accumulator
 // with mixed additions (variant V, curve.hpp).  Software pipeline: the

@@ -63,6 +63,7 @@ struct FixedTable {
   uint32_t* d = nullptr;
   size_t bytes = 0;
   uint8_t* inf = nullptr;  // [n_t] infinite SRS points (skipped)
+  bool any_inf = true;     // some flag of inf is set (else the kernels get no flags)
 };
 
 // optional per-kernel timing with HIP events on the launch stream

@@ -186,7 +186,7 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
   const uint32_t g = t / n_pad, i = t - g * n_pad;
   const int w0 = (int)g * WG, w1 = w0 + WG < W ? w0 + WG : W;
   Xyzz<C> acc = xyzz_inf<C>();
-  if (i < n && !inf[i]) {
+  if (i < n && !(inf != nullptr && inf[i] != 0)) {
     const uint32_t* sc = scalars + (size_t)b * stride_words + (size_t)i * 8;
     uint32_t s[8];
     {
@@ -271,13 +271,10 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
     uint32_t s[8], carry = 0;
     bool skip = false;  // infinity SRS point: all its terms are the identity
     auto load = [&](uint32_t ii) {
-      const uint4 lo = reinterpret_cast<const uint4*>(sc + (size_t)ii * 8)[0];
-      const uint4 hi = reinterpret_cast<const uint4*>(sc + (size_t)ii * 8)[1];
-      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
-      s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+      scalar_load(sc + (size_t)ii * 8, s);
       scalar_reduce<C>(s);
       carry = 0;
-      skip = inf[ii] != 0;
+      skip = inf != nullptr && inf[ii] != 0;
     };
     load(i);
 #pragma unroll 1
@@ -360,6 +357,9 @@ static TabStrides tab_strides(const FixedTable& ft) {
   return fixed_strides<C>(ft.point_major, ft.W, ft.n_t, 1ull << (ft.c - 1));
 }
 
+// the infinity flags the accumulation kernels read, or null when none is set
+static const uint8_t* fixed_inf(const FixedTable& ft) { return ft.any_inf ? ft.inf : nullptr; }
+
 template <class C>
 static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   FixedTable& ft = ctx->fixed;
@@ -414,6 +414,15 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
     KZGX_TRY_HIP(hipGetLastError());
     KZGX_TRY_HIP(hipStreamSynchronize(st));
   }
+  // whether any SRS point of the prefix is infinite: when none is (every SRS
+  // but a degenerate tau = 0 one), the accumulation kernels get no flag array
+  // and read no flag per point
+  {
+    std::vector<uint8_t> h(n);
+    KZGX_TRY_HIP(hipMemcpyAsync(h.data(), d_inf, n, hipMemcpyDeviceToHost, st));
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+    ft.any_inf = std::any_of(h.begin(), h.end(), [](uint8_t v) { return v != 0; });
+  }
   g.ok = true;
   ft.inf = d_inf;
   ft.c = c;
@@ -461,7 +470,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
     KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
-                       (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), ft.inf, WG, Q, wsp->fpart);
+                       (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), WG, Q, wsp->fpart);
     hipLaunchKernelGGL(k_fixed_fold_finish<C>, dim3((unsigned)batch), dim3(64), 0, st, wsp->fpart, Q, d_out,
                        d_out_inf);
     KZGX_TRY_HIP(hipGetLastError());
@@ -494,7 +503,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
       {
         ProfScope p(ctx, st, "msm_accum");
         hipLaunchKernelGGL((k_fixed_accum_flat<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                           (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), ft.inf, Q, T, ws.fpart);
+                           (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), Q, T, ws.fpart);
       }
       ProfScope p(ctx, st, "msm_reduce");
       // T / 64 wavefront partials per MSM: one more 64:1 level, then one
@@ -529,7 +538,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   {
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                       (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), ft.inf, T, ws.fpart);
+                       (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), T, ws.fpart);
   }
   if (wave_red) {
     ProfScope p(ctx, st, "msm_reduce");

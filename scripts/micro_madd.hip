@@ -93,7 +93,16 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
   uint8_t* d_inf;
   hipMalloc(&d_pts, 64 * affine_words<C>() * 4);
   hipLaunchKernelGGL(k_points<C>, dim3(1), dim3(64), 0, 0, d_pts);
-  if (hipMalloc(&d_tab, entries * PW * 4) != hipSuccess) return 2;
+  // MICRO_CONTIG=1: the table as one physically contiguous allocation (fewer,
+  // larger page-table fragments: the TLB-reach probe)
+  if (getenv("MICRO_CONTIG")) {
+    if (hipExtMallocWithFlags((void**)&d_tab, entries * PW * 4, hipDeviceMallocContiguous) != hipSuccess) {
+      printf("{\"contiguous_alloc\": \"failed\", \"bytes\": %zu}\n", entries * PW * 4);
+      return 2;
+    }
+  } else if (hipMalloc(&d_tab, entries * PW * 4) != hipSuccess) {
+    return 2;
+  }
   hipLaunchKernelGGL(k_fill<C>, dim3(65536), dim3(256), 0, 0, d_tab, entries, d_pts);
   std::vector<uint32_t> sc((size_t)B * n * 8);
   uint64_t x = 0x9E3779B97F4A7C15ull;
@@ -120,13 +129,13 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
       hipEventRecord(e0, 0);
       if (v == 0)
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, d_inf, T, d_p0);
+                           ts, nullptr, T, d_p0);
       else if (v == 1)
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 1, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, d_inf, T, d_p1);
+                           ts, nullptr, T, d_p1);
       else  // loads and digit recoding only: the memory path's own rate
         hipLaunchKernelGGL((k_fixed_accum<C, CB, 2, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, d_inf, T, d_p0 + 0 * pw);
+                           ts, nullptr, T, d_p0 + 0 * pw);
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float m = 0;
@@ -247,6 +256,12 @@ int main() {
   bad |= run_accum<BN254G1, 12, 0>("BN254", 2048, 22);
   bad |= run_accum<BLS12381G1, 12, 1>("BLS12381", 2048, 65);
   bad |= run_accum<BLS12381G1, 12, 0>("BLS12381", 2048, 65);
+  if (getenv("MICRO_C14")) bad |= run_accum<BN254G1, 14, 1>("BN254", 2048, 22);
+  if (getenv("MICRO_CSWEEP")) {  // table window sweep: HBM gather (c = 8, 12) vs a cache-resident table (c = 2, 4)
+    bad |= run_accum<BN254G1, 2, 1>("BN254", 2048, 22);
+    bad |= run_accum<BN254G1, 4, 1>("BN254", 2048, 22);
+    bad |= run_accum<BN254G1, 8, 1>("BN254", 2048, 22);
+  }
   if (getenv("MICRO_CHAINS")) {
     for (int w : {1, 2, 3, 4}) {
       run_chain<1>(w);
