@@ -309,6 +309,25 @@ def timed_run(ctx, step, streams, steps, warmup, world, dist, torch, dev):
     return elapsed, kern
 
 
+def clock_during(ctx, step, step_s, torch, dev, nsteps=4):
+    """core GHz while `step` runs: the probe (kzgx_clock_probe) is enqueued
+    first on a stream of its own, so it is resident before the step's kernels
+    fill the GPU, and spins for about half of nsteps steps"""
+    try:
+        buf = torch.zeros(3, dtype=torch.int64, device=dev)
+        ps = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize(dev)
+        ctx.clock_probe(buf.data_ptr(), max(1000, int(step_s * 1e6 * nsteps / 2)), ps.cuda_stream)
+        for _ in range(nsteps):
+            step()
+        torch.cuda.synchronize(dev)
+        core, wall, khz = (int(v) for v in buf.cpu().tolist())
+        return core / wall * khz * 1e-6 if wall else None
+    except Exception as e:  # noqa: BLE001 -- a measurement aid, never fatal
+        print("bench: clock probe unavailable: %s" % e, file=sys.stderr)
+        return None
+
+
 def median_ms(f, reps):
     f()  # warm (workspaces, first-use tables)
     ts = []
@@ -509,6 +528,11 @@ def main():
 
     elapsed, kern = timed_run(ctx, step, streams, args.steps, args.warmup, world, dist, torch, dev)
 
+    # ---- core clock during the step (outside the timed region): a one-wave
+    # probe spins on its own stream beside a few more steps (DVFS lowers the
+    # clock under this load: profiles/r03_pmc_clock_table_sweep.json) ----
+    step_clock = clock_during(ctx, step, elapsed / args.steps, torch, dev)
+
     # ---- parity: every output of the last step (oracle identity, MSM-independent) ----
     checked = ok = 0
     bad = None
@@ -611,9 +635,10 @@ def main():
         madd_rate = madds / (ms_per_step * 1e-3)
         peak = None
         mad_peak = None
+        mad_ghz = None
         try:
             peak = ctx.microbench_mixed_add()
-            mad_peak = ctx.microbench_mad_u64()
+            mad_peak, mad_ghz = ctx.microbench_mad_u64_clock()
         except Exception as e:  # noqa: BLE001 -- reported, never fatal for the headline
             print("bench: VALU microbenchmarks unavailable: %s" % e, file=sys.stderr)
         if curve_pts is not None and fb[0]:
@@ -688,6 +713,14 @@ def main():
                     "peak_mad_lane_ops_per_s": mad_peak,
                     "frac": madd_rate * mpa / mad_peak,
                     "valu_per_mixed_add_isa": isa,
+                    "clock_ghz": {"step": step_clock, "peak_run": mad_ghz},
+                    "frac_at_step_clock": (madd_rate * mpa / step_clock) / (mad_peak / mad_ghz)
+                    if step_clock and mad_ghz else None,
+                    "clock_from": "kzgx_clock_probe: one wave counting core clocks against the 100 MHz wall "
+                                  "clock, resident beside 4 more steps (outside the timed region); the peak's "
+                                  "own launch stamps its clock the same way. The chip lowers its clock under "
+                                  "this load (DVFS), so frac_at_step_clock is the issue efficiency at the "
+                                  "clock the step actually ran",
                     "peak_from": "kzgx_microbench_mad_u64: v_mad_u64_u32 in asm, 8 independent chains per lane, "
                                  "whole GPU, measured live (the hardware issue ceiling of the instruction every "
                                  "partial product is)",

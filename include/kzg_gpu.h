@@ -127,6 +127,15 @@ int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s);
  * operations per second; 8 independent chains per lane, whole GPU) -- the
  * denominator of the bench's mad_issue roofline */
 int kzgx_microbench_mad_u64(kzgx_ctx* ctx, double* lane_ops_per_s);
+/* the same, plus the core clock (GHz) the ceiling ran at: one lane of the
+ * launch counts core clocks against the constant-rate wall clock */
+int kzgx_microbench_mad_u64_clock(kzgx_ctx* ctx, double* lane_ops_per_s, double* core_ghz);
+/* measurement: enqueue on stream (NULL = the context's) a one-wavefront
+ * probe that spins for spin_us of wall time and writes three uint64 to the
+ * device buffer d_out: core clocks elapsed, wall ticks elapsed, wall clock
+ * rate (kHz).  Enqueued beside a running batch it reads that batch's clock
+ * (the DVFS clock is one per device); it occupies one wave slot. */
+int kzgx_clock_probe(kzgx_ctx* ctx, void* stream, unsigned spin_us, void* d_out);
 
 /* ---- SRS ---------------------------------------------------------------- */
 /* upload n canonical affine points as the G1 SRS (replaces any previous one) */

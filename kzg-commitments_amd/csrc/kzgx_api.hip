@@ -294,7 +294,20 @@ int kzgx_microbench_mad_u64(kzgx_ctx* ctx, double* lane_ops_per_s) {
   KZGX_TRY(activate(ctx));
   if (!lane_ops_per_s) return KZGX_ERR_ARG;
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
-  return kzgx::microbench_mad_u64(&ctx->c, lane_ops_per_s);
+  return kzgx::microbench_mad_u64(&ctx->c, lane_ops_per_s, nullptr);
+}
+
+int kzgx_microbench_mad_u64_clock(kzgx_ctx* ctx, double* lane_ops_per_s, double* core_ghz) {
+  KZGX_TRY(activate(ctx));
+  if (!lane_ops_per_s || !core_ghz) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return kzgx::microbench_mad_u64(&ctx->c, lane_ops_per_s, core_ghz);
+}
+
+int kzgx_clock_probe(kzgx_ctx* ctx, void* stream, unsigned spin_us, void* d_out) {
+  KZGX_TRY(activate(ctx));
+  if (!d_out || spin_us == 0 || spin_us > 10000000u) return KZGX_ERR_ARG;
+  return kzgx::clock_probe(&ctx->c, pick(ctx, stream), spin_us, static_cast<uint64_t*>(d_out));
 }
 
 int kzgx_microbench_mixed_add(kzgx_ctx* ctx, double* adds_per_s) {

@@ -166,7 +166,8 @@ int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
 // mixed additions / s of the fixed-base accumulation loop on L1-resident operands (msm_fixed.hip)
 int microbench_mixed_add(Ctx* ctx, double* rate);
-int microbench_mad_u64(Ctx* ctx, double* rate);
+int microbench_mad_u64(Ctx* ctx, double* rate, double* ghz);
+int clock_probe(Ctx* ctx, hipStream_t st, uint32_t spin_us, uint64_t* d_out);
 size_t fixed_table_bytes(int curve, int c, size_t n);
 int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res);  // ns, core clocks per op
 // one workgroup sums count XYZZ points -> canonical affine (msm.hip)

@@ -688,7 +688,16 @@ static int microbench_madd_impl(Ctx* ctx, double* rate) {
 // v_mad_u64_u32 issue ceiling: 8 independent accumulator chains per lane,
 // 256 mads per chain per iteration, 8 waves per SIMD (the instruction
 // exactly, in asm; scripts/micro_valu.hip, profiles/r01_micro_valu.txt)
-__global__ __launch_bounds__(256) void k_microbench_mad64(uint32_t iters, uint32_t* __restrict__ sink) {
+__global__ __launch_bounds__(256) void k_microbench_mad64(uint32_t iters, uint32_t* __restrict__ sink,
+                                                          uint64_t* __restrict__ stamp) {
+  // block 0's first lane counts core clocks against the constant-rate wall
+  // clock over its run: every block is resident at once, so that is the
+  // clock the ceiling was measured at
+  uint64_t w0 = 0, c0 = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w0 = wall_clock64();
+    c0 = clock64();
+  }
   uint64_t acc[8];
   const uint32_t a = threadIdx.x + 1, b = blockIdx.x + 3;
 #pragma unroll
@@ -708,29 +717,67 @@ __global__ __launch_bounds__(256) void k_microbench_mad64(uint32_t iters, uint32
 #pragma unroll
   for (int k = 0; k < 8; k++) o ^= acc[k];
   if ((uint32_t)o == 0x9e3779b9u) sink[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)o;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t c1 = clock64(), w1 = wall_clock64();
+    stamp[0] = c1 - c0;
+    stamp[1] = w1 - w0;
+  }
 }
 
-int microbench_mad_u64(Ctx* ctx, double* rate) {
+int microbench_mad_u64(Ctx* ctx, double* rate, double* ghz) {
   hipStream_t st = ctx->stream;
   const uint32_t blocks = 256 * 8, iters = 64;
   uint32_t* d_sink = nullptr;
-  KZGX_TRY_HIP(hipMalloc((void**)&d_sink, (size_t)blocks * 256 * 4));
-  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, 2u, d_sink);  // warm
+  KZGX_TRY_HIP(hipMalloc((void**)&d_sink, (size_t)blocks * 256 * 4 + 16));
+  uint64_t* d_stamp = reinterpret_cast<uint64_t*>(d_sink + (size_t)blocks * 256);
+  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, 2u, d_sink, d_stamp);  // warm
   hipEvent_t a, b;
   KZGX_TRY_HIP(hipEventCreate(&a));
   KZGX_TRY_HIP(hipEventCreate(&b));
   KZGX_TRY_HIP(hipEventRecord(a, st));
-  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, iters, d_sink);
+  hipLaunchKernelGGL(k_microbench_mad64, dim3(blocks), dim3(256), 0, st, iters, d_sink, d_stamp);
   KZGX_TRY_HIP(hipEventRecord(b, st));
   KZGX_TRY_HIP(hipEventSynchronize(b));
   float ms = 0;
   hipError_t e = hipEventElapsedTime(&ms, a, b);
+  uint64_t h[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemcpy(h, d_stamp, sizeof h, hipMemcpyDeviceToHost);
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   (void)hipFree(d_sink);
   KZGX_TRY_HIP(e);
   KZGX_TRY_HIP(hipGetLastError());
   *rate = (double)blocks * 256 * iters * 256 / (ms * 1e-3);
+  if (ghz) {
+    int khz = 0;
+    KZGX_TRY_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+    *ghz = h[1] ? (double)h[0] / (double)h[1] * khz * 1e-6 : 0.0;
+  }
+  return KZGX_OK;
+}
+
+// The core clock while other work runs: one lane spins for spin_us of the
+// constant-rate wall clock and counts core clocks meanwhile.  The DVFS clock
+// is one per device (MI355X_MICROARCH.md, DVFS give-back), so a probe
+// resident beside a kernel reads that kernel's clock; it holds one wave slot.
+// out: core clocks, wall ticks, wall clock rate in kHz.
+__global__ __launch_bounds__(64) void k_clock_probe(uint64_t ticks, uint32_t khz, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const uint64_t w0 = wall_clock64(), c0 = clock64();
+  uint64_t w = w0;
+  while (w - w0 < ticks) w = wall_clock64();
+  const uint64_t c1 = clock64();
+  out[0] = c1 - c0;
+  out[1] = w - w0;
+  out[2] = khz;
+}
+
+int clock_probe(Ctx* ctx, hipStream_t st, uint32_t spin_us, uint64_t* d_out) {
+  int khz = 0;
+  KZGX_TRY_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+  const uint64_t ticks = (uint64_t)spin_us * (uint64_t)khz / 1000;
+  hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, st ? st : ctx->stream, ticks, (uint32_t)khz, d_out);
+  KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }
 

@@ -24,7 +24,7 @@ EXPORTS = [
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
     "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout",
-    "kzgx_microbench_mad_u64", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_microbench_mad_u64", "kzgx_microbench_mad_u64_clock", "kzgx_clock_probe", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device",
@@ -83,6 +83,9 @@ def lib():
             "kzgx_set_fixed_base_layout": (ctypes.c_int, [vp, ctypes.c_int]),
             "kzgx_fixed_base_layout": (ctypes.c_int, [vp, intp]),
             "kzgx_microbench_mad_u64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+            "kzgx_microbench_mad_u64_clock": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                                             ctypes.POINTER(ctypes.c_double)]),
+            "kzgx_clock_probe": (ctypes.c_int, [vp, vp, ctypes.c_uint, vp]),
             "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_microbench_mixed_add": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
@@ -235,6 +238,19 @@ class Context:
         r = ctypes.c_double(0)
         _chk(lib().kzgx_microbench_mad_u64(self.h, ctypes.byref(r)), "kzgx_microbench_mad_u64")
         return r.value
+
+    def microbench_mad_u64_clock(self):
+        """(v_mad_u64_u32 lane operations / s, core GHz the ceiling ran at)"""
+        r = ctypes.c_double(0)
+        g = ctypes.c_double(0)
+        _chk(lib().kzgx_microbench_mad_u64_clock(self.h, ctypes.byref(r), ctypes.byref(g)),
+             "kzgx_microbench_mad_u64_clock")
+        return r.value, g.value
+
+    def clock_probe(self, d_out: int, spin_us: int, stream: int = 0):
+        """enqueue the core-clock probe on stream; d_out: device address of 3 uint64"""
+        _chk(lib().kzgx_clock_probe(self.h, ctypes.c_void_p(stream or None), spin_us, ctypes.c_void_p(d_out)),
+             "kzgx_clock_probe")
 
     def set_fixed_points_per_thread(self, p: int):
         _chk(lib().kzgx_set_fixed_points_per_thread(self.h, p), "kzgx_set_fixed_points_per_thread")

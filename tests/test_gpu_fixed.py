@@ -299,3 +299,28 @@ def test_microbench_mad_u64_is_a_hardware_ceiling():
         assert 1.0e13 < r < 4.0e13, r
     finally:
         ctx.close()
+
+
+def test_clock_measurements_read_a_plausible_core_clock():
+    """kzgx_microbench_mad_u64_clock and kzgx_clock_probe: the core clock from
+    core-clock vs wall-clock counters (MI355X: up to 2.4 GHz, DVFS lowers it
+    under load); the probe's wall time is the spin asked for"""
+    import torch
+    import kzgx
+    import kzg_ref as K
+    ctx = kzgx.Context("BN254")
+    try:
+        ctx.gen_srs(K.default_tau(K.BN254), 8)
+        r, ghz = ctx.microbench_mad_u64_clock()
+        assert 1.0e13 < r < 4.0e13, r
+        assert 0.5 < ghz < 3.0, ghz
+        buf = torch.zeros(3, dtype=torch.int64, device="cuda:0")
+        ctx.clock_probe(buf.data_ptr(), 2000)
+        torch.cuda.synchronize()
+        core, wall, khz = (int(v) for v in buf.cpu().tolist())
+        assert khz > 0 and abs(wall / khz - 2.0) < 0.1, (wall, khz)  # 2000 us of wall ticks
+        assert 0.5 < core / wall * khz * 1e-6 < 3.0, (core, wall, khz)
+        with pytest.raises(kzgx.KzgxError):
+            ctx.clock_probe(buf.data_ptr(), 0)
+    finally:
+        ctx.close()
