@@ -45,6 +45,14 @@
 #define KZGX_GROUP_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
 
+// the full XYZZ addition with its products as lockstep chains (1) or one
+// product at a time (0, the default: the lockstep form measured no change in
+// single-call latency -- 0.746 / 0.296 ms Pippenger / table commit against
+// 0.741 / 0.301 -- nor in the batched Pippenger leg, profiles/r03_add_tri_latency.txt)
+#ifndef KZGX_ADD_TRI
+#define KZGX_ADD_TRI 0
+#endif
+
 namespace kzgx {
 
 template <class C>
@@ -301,6 +309,31 @@ KZGX_DEV Xyzz<C> xyzz_add_impl(const Xyzz<C>& p, const Xyzz<C>& q) {
   using F = typename C::Fp29;
   if (xyzz_is_inf<C>(p)) return q;
   if (xyzz_is_inf<C>(q)) return p;
+#if KZGX_ADD_TRI
+  // the same formulas and bounds as below, the products three chains in
+  // lockstep (field29.hpp "three chains"): (U1, U2, S1), (S2, ZZ1 ZZ2,
+  // ZZZ1 ZZZ2), (P^2, R^2) paired, (PPP, Q, ZZ3), then Y3 with ZZZ3
+  {
+    F29<F> U1, U2, S1, S2, ZZ12, ZZZ12;
+    f29_mul_x3<F>(p.X, q.ZZ, q.X, p.ZZ, p.Y, q.ZZZ, U1, U2, S1);
+    f29_mul_x3<F>(q.Y, p.ZZZ, p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, S2, ZZ12, ZZZ12);
+    const F29<F> P = f29_sub<F>(U2, U1, F::P2);  // < 4m
+    const F29<F> R = f29_sub<F>(S2, S1, F::P2);  // < 4m
+    F29<F> PP, RR;
+    f29_sqr_x2_pair<F>(P, R, PP, RR);
+    if (f29_is_zero_lt2m<F>(PP)) {
+      if (f29_is_zero<F>(R)) return xyzz_dbl_impl<C>(p);
+      return xyzz_inf<C>();
+    }
+    F29<F> PPP, Q;
+    Xyzz<C> r;
+    f29_mul_x3<F>(P, PP, U1, PP, ZZ12, PP, PPP, Q, r.ZZ);
+    r.X = f29_sub<F>(RR, f29_add<F>(PPP, f29_add<F>(Q, Q)), F::P6);
+    f29_mul2_mul<F>(R, f29_sub<F>(Q, r.X, F::P8), f29_sub<F>(f29_zero<F>(), S1, F::P2), PPP, ZZZ12, PPP, r.Y,
+                    r.ZZZ);  // Y3 < 2m
+    return r;
+  }
+#endif
   F29<F> U1 = f29_mul<F>(p.X, q.ZZ);
   F29<F> U2 = f29_mul<F>(q.X, p.ZZ);
   F29<F> S1 = f29_mul<F>(p.Y, q.ZZZ);

@@ -442,6 +442,27 @@ KZGX_DEV void f29_mul_x3(const F29<F>& a0, const F29<F>& b0, const F29<F>& a1, c
   });
 }
 
+// f29_sqr_x2 with the two chains in lockstep (mad_pair) whatever
+// KZGX_MAD_PAIR says: for latency-bound callers (few waves per SIMD), where
+// a lone chain pays every hazard pad
+template <class F>
+KZGX_DEV void f29_sqr_x2_pair(const F29<F>& a0, const F29<F>& a1, F29<F>& r0, F29<F>& r1) {
+  F29<F> d0, d1;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) {
+    d0.v[i] = a0.v[i] << 1;
+    d1.v[i] = a1.v[i] << 1;
+  }
+  const PLimbs<F> pl;
+  MontChain<F> c0, c1;
+  c0.acc = c1.acc = 0;
+  static_for<0, 2 * F::L - 1>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    mc_sqr2<F, k>(c0, a0, d0, c1, a1, d1);
+    mc_reduce2<F, k>(c0, r0, c1, r1, pl.v);
+  });
+}
+
 // r0 = (a b + c d) / R with one reduction, r1 = e f / R.  The products run as
 // three chains in lockstep (c d into a second accumulator of r0 that starts
 // from zero every column and is merged before the column's reduction), the
