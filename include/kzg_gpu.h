@@ -84,6 +84,12 @@ int kzgx_prof_clear(kzgx_ctx* ctx);
  * settable only before the SRS is loaded; entries per accumulation thread */
 int kzgx_set_window_bits(kzgx_ctx* ctx, int c);
 int kzgx_set_segment(kzgx_ctx* ctx, unsigned k);
+/* tuning: table-less MSM batches of at most max_batch MSMs (default 16; 0 =
+ * never) over the first 65536 SRS points run at window 10 on a second window
+ * table built with the SRS: a single commit's bucket reduction is a chain of
+ * dependent additions as deep as the bucket count, so the shorter window
+ * answers one call sooner (BN254 degree 4096: 0.545 vs 0.712 ms) */
+int kzgx_set_small_batch(kzgx_ctx* ctx, unsigned max_batch);
 
 /* fixed-base precomputation (the SRS is fixed for a trusted_setup's
  * lifetime): store M[w][i][j] = (j+1) 2^(c w) SRS[i] for the first n_points

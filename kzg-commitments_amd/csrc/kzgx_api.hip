@@ -144,7 +144,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->c.stream);
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
-  void* bufs[] = {c.d_table, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
+  void* bufs[] = {c.d_table, c.d_table_small, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
                   c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw, ctx->d_g2tab};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -215,6 +215,13 @@ int kzgx_set_window_bits(kzgx_ctx* ctx, int c) {
   if (ctx->c.n_srs != 0) return KZGX_ERR_ARG;  // the fixed-base table depends on c
   ctx->c.c = c;
   ctx->c.W = (257 + c - 1) / c;
+  return KZGX_OK;
+}
+
+int kzgx_set_small_batch(kzgx_ctx* ctx, unsigned max_batch) {
+  KZGX_TRY(activate(ctx));
+  if (max_batch > 65535) return KZGX_ERR_ARG;
+  ctx->c.small_batch = max_batch;
   return KZGX_OK;
 }
 

@@ -72,6 +72,11 @@ struct ProfRec {
   hipEvent_t a, b;
 };
 
+// batches of at most this many MSMs use the small-window table (msm.hip)
+#ifndef KZGX_SMALL_BATCH
+#define KZGX_SMALL_BATCH 16
+#endif
+
 struct Ctx {
   int curve = 0;
   int device = 0;
@@ -82,6 +87,12 @@ struct Ctx {
   size_t n_srs = 0;
   uint32_t* d_table = nullptr;  // [W][n_srs] affine Montgomery points
   size_t table_bytes = 0;
+  // small-batch window table (msm.hip, msm_batch_c): [W_s][n_small] at
+  // window KZGX_SMALL_WINDOW_BITS over the first n_small SRS points
+  uint32_t* d_table_small = nullptr;
+  size_t table_small_bytes = 0;
+  size_t n_small = 0;
+  size_t small_batch = KZGX_SMALL_BATCH;  // largest batch that uses it (0: never)
   uint8_t* d_inf = nullptr;  // [n_srs]
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];

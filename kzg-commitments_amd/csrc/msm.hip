@@ -623,6 +623,20 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
 // --------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------
+// Small batches (a single create_commit / create_proof, the reference's own
+// call pattern) are latency-bound: the bucket reduction of one MSM is a chain
+// of dependent additions whose depth grows with the bucket count 2^(c-1).
+// Measured single degree-4096 BN254 commits (host buffers,
+// profiles/r03_latency_window.json): c = 10 0.545 ms, c = 11 0.587, c = 12
+// 0.712, c = 13 0.679; batched throughput keeps c = 12.  So the context also
+// keeps a c = 10 window table over the first SMALL_MAX_POINTS SRS points
+// (8.5 MB for a 4097-point SRS, 136 MB at most), used for batches of at most
+// Ctx::small_batch MSMs (kzgx_set_small_batch; 0 = never) inside that prefix.
+#ifndef KZGX_SMALL_WINDOW_BITS
+#define KZGX_SMALL_WINDOW_BITS 10
+#endif
+constexpr size_t SMALL_MAX_POINTS = 65536;
+
 template <class C>
 int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   const int W = ctx->W;
@@ -633,6 +647,20 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   hipLaunchKernelGGL(k_srs_to_mont<C>, grd, blk, 0, ctx->stream, d_canon, ctx->d_table, ctx->d_inf, (uint32_t)n);
   hipLaunchKernelGGL(k_table_build<C>, grd, blk, 0, ctx->stream, ctx->d_table, ctx->d_inf, (uint32_t)n, W, ctx->c);
   KZGX_TRY_HIP(hipGetLastError());
+  ctx->n_small = 0;
+  if (ctx->c != KZGX_SMALL_WINDOW_BITS) {
+    // window 0 of the small table is the Montgomery SRS prefix (window 0 of
+    // the main table); k_table_build derives the others
+    const size_t ns = n < SMALL_MAX_POINTS ? n : SMALL_MAX_POINTS;
+    constexpr int WS = Win<KZGX_SMALL_WINDOW_BITS>::W;
+    KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_small, (size_t)WS * ns * pw, &ctx->table_small_bytes));
+    KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_small, ctx->d_table, ns * pw, hipMemcpyDeviceToDevice, ctx->stream));
+    dim3 grs((unsigned)((ns + 255) / 256));
+    hipLaunchKernelGGL(k_table_build<C>, grs, blk, 0, ctx->stream, ctx->d_table_small, ctx->d_inf, (uint32_t)ns, WS,
+                       KZGX_SMALL_WINDOW_BITS);
+    KZGX_TRY_HIP(hipGetLastError());
+    ctx->n_small = ns;
+  }
   ctx->n_srs = n;
   return fixed_build(ctx, d_canon, n);
 }
@@ -640,7 +668,7 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
 template <class C, int CB>
 int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
                    uint32_t* d_out_inf, hipStream_t st, uint32_t point_base, uint32_t point_stride,
-                   uint32_t* xyzz_out) {
+                   uint32_t* xyzz_out, const uint32_t* d_tab, size_t n_rows) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   const size_t emax = (size_t)n * W;
@@ -691,12 +719,12 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   {
     ProfScope p(ctx, st, "msm_scatter");
     hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
-                       ws.counts, ws.cursors, (uint32_t)nblk, ws.entries, emax, (uint32_t)ctx->n_srs, point_base, point_stride);
+                       ws.counts, ws.cursors, (uint32_t)nblk, ws.entries, emax, (uint32_t)n_rows, point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL(k_msm_accum<C>, dim3((unsigned)((smax + 255) / 256), (unsigned)batch), blk, 0, st, ws.entries,
-                       emax, ws.offsets, NB, ctx->d_table, K, (uint32_t)smax, ws.bsum, ws.heads, ws.tails, ws.tailk,
+                       emax, ws.offsets, NB, d_tab, K, (uint32_t)smax, ws.bsum, ws.heads, ws.tails, ws.tailk,
                        ws.sstate);
   }
   {
@@ -744,11 +772,19 @@ template <class C>
 static int msm_batch_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
                        uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t point_base,
                        uint32_t point_stride, uint32_t* xyzz_out) {
+  // small batches inside the small table's prefix: the short-reduction window
+  const size_t last = (size_t)point_base + (batch ? (batch - 1) * (size_t)point_stride : 0) + n;
+  if (ctx->n_small && batch <= ctx->small_batch && last <= ctx->n_small)
+    return msm_batch_impl<C, KZGX_SMALL_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st,
+                                                     point_base, point_stride, xyzz_out, ctx->d_table_small,
+                                                     ctx->n_small);
+  const uint32_t* T = ctx->d_table;
+  const size_t R = ctx->n_srs;
   switch (ctx->c) {
-    case 10: return msm_batch_impl<C, 10>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
-    case 11: return msm_batch_impl<C, 11>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
-    case 12: return msm_batch_impl<C, 12>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
-    case 13: return msm_batch_impl<C, 13>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out);
+    case 10: return msm_batch_impl<C, 10>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out, T, R);
+    case 11: return msm_batch_impl<C, 11>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out, T, R);
+    case 12: return msm_batch_impl<C, 12>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out, T, R);
+    case 13: return msm_batch_impl<C, 13>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, point_base, point_stride, xyzz_out, T, R);
     default: return KZGX_ERR_INTERNAL;
   }
 }

@@ -24,7 +24,7 @@ EXPORTS = [
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
     "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout",
-    "kzgx_microbench_mad_u64", "kzgx_microbench_mad_u64_clock", "kzgx_clock_probe", "kzgx_set_fixed_points_per_thread", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
+    "kzgx_microbench_mad_u64", "kzgx_microbench_mad_u64_clock", "kzgx_clock_probe", "kzgx_set_fixed_points_per_thread", "kzgx_set_small_batch", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
     "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device",
@@ -87,6 +87,7 @@ def lib():
                                                              ctypes.POINTER(ctypes.c_double)]),
             "kzgx_clock_probe": (ctypes.c_int, [vp, vp, ctypes.c_uint, vp]),
             "kzgx_set_fixed_points_per_thread": (ctypes.c_int, [vp, ctypes.c_uint]),
+            "kzgx_set_small_batch": (ctypes.c_int, [vp, ctypes.c_uint]),
             "kzgx_microbench_mixed_add": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_load_srs_g1": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_gen_srs_g1": (ctypes.c_int, [vp, u64p, sz, sz]),
@@ -199,6 +200,10 @@ class Context:
 
     def set_window_bits(self, c: int):
         _chk(lib().kzgx_set_window_bits(self.h, c), "kzgx_set_window_bits")
+
+    def set_small_batch(self, max_batch: int):
+        """table-less batches of <= max_batch MSMs use the window-10 table (0 = never)"""
+        _chk(lib().kzgx_set_small_batch(self.h, max_batch), "kzgx_set_small_batch")
 
     def set_segment(self, k: int):
         _chk(lib().kzgx_set_segment(self.h, k), "kzgx_set_segment")

@@ -309,3 +309,30 @@ def test_prove_range_long_polynomial_few_points(name, C, npts, oracle_c):
         assert dt < 2.0, dt
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_small_batch_window_matches_main_window(name, C, ctx_factory):
+    """Batches of <= kzgx_set_small_batch MSMs run on the window-10 table
+    (msm.hip, the single-call latency path); larger ones, and every batch
+    with it off, on the context's window-12 table.  Both must give [P(tau)]G1
+    for every MSM, at the threshold (16) and one past it, with the digit
+    edge cases (0, 1, r - 1) and a zero polynomial in the batch."""
+    ctx = ctx_factory(name)
+    tau = K.default_tau(C)
+    n = 4097
+    ctx.gen_srs(tau, 5000)
+    polys = [K.random_scalars(C, n, seed=500 + b) for b in range(17)]
+    polys[0][:3] = [0, 1, C.r - 1]
+    polys[3] = [0] * n
+    S = np.concatenate([limbs(p) for p in polys])
+    exp = [K.commit_via_tau(C, tau, p) for p in polys]
+    for small in (16, 0):
+        ctx.set_small_batch(small)
+        for batch in (1, 16, 17):
+            out, inf = ctx.msm_batch(S, n, batch)
+            for b in range(batch):
+                got = pt(name, out[b], inf[b])
+                assert got == exp[b], (small, batch, b)
+    with pytest.raises(Exception):
+        ctx.set_small_batch(1 << 20)
