@@ -422,25 +422,30 @@ __global__ __launch_bounds__(64) void k_msm_wg_fixup(uint32_t nb, uint32_t nwg, 
   xyzz_store<C>(bsum + ((size_t)b * nb + k) * XW, acc);
 }
 
-// pass 5a: bucket running sums, J = RED_J buckets per thread.  Thread t of
+// pass 5a: bucket running sums, J buckets per thread.  Thread t of
 // MSM b owns buckets [t J, t J + J) and emits
 //   R_t = sum_j (j + 1) B_{tJ+j}   and   T_t = sum_j B_{tJ+j}
 // so that sum_k (k + 1) B_k = sum_t R_t + J sum_t t T_t.
+// J = RED_J for batches; RED_J_SMALL for small batches, whose reduction is
+// latency-bound: every lane is alone on its SIMD and issues its additions one
+// after another, so the fewer per lane the sooner the call returns (the fold
+// then runs as one workgroup with the affine conversion inline)
 constexpr uint32_t RED_J = 8;
+constexpr uint32_t RED_J_SMALL = 2;
 
-template <class C>
+template <class C, uint32_t J>
 __global__ __launch_bounds__(256, KZGX_BS_WAVES) void k_msm_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb,
                                                                         const uint32_t* __restrict__ bsum,
                                                                         uint32_t* __restrict__ rt) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y;
-  const uint32_t T1 = nb / RED_J;
+  const uint32_t T1 = nb / J;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T1) return;
-  const uint32_t* off = offsets + (size_t)b * (nb + 1) + t * RED_J;
-  const uint32_t* src = bsum + ((size_t)b * nb + t * RED_J) * XW;
+  const uint32_t* off = offsets + (size_t)b * (nb + 1) + t * J;
+  const uint32_t* src = bsum + ((size_t)b * nb + t * J) * XW;
   Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
-  for (int j = (int)RED_J - 1; j >= 0; j--) {
+  for (int j = (int)J - 1; j >= 0; j--) {
     if (off[j + 1] > off[j]) run = xyzz_add_impl<C>(run, xyzz_load<C>(src + (size_t)j * XW));  // empty buckets: never written
     sum = xyzz_add_impl<C>(sum, run);
   }
@@ -481,7 +486,7 @@ KZGX_DEV Xyzz<C> xyzz_dbl_n(Xyzz<C> p, uint32_t m) {  // 2^log2(m) p, m a power 
 // U_l = R'_l + J G S_l (l >= 1) is then summed by a 6-step shuffle tree, and
 // lane 0 stores V as an XYZZ point (k_msm_finish converts it, or chunked
 // callers sum it with k_xyzz_sum).  Four MSMs per 256-thread block.
-template <class C>
+template <class C, uint32_t RED_J>
 __global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restrict__ rt, uint32_t T1, uint32_t batch,
                                                          uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(256) void k_msm_bucket_fold(const uint32_t* __restr
 // separate finish launch).
 constexpr int FOLD_WG = 256;
 
-template <class C>
+template <class C, uint32_t RED_J>
 __global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* __restrict__ rt, uint32_t T1,
                                                                 uint32_t* __restrict__ xyzz_out,
                                                                 uint32_t* __restrict__ out,
@@ -636,6 +641,10 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
 #define KZGX_SMALL_WINDOW_BITS 10
 #endif
 constexpr size_t SMALL_MAX_POINTS = 65536;
+// batches of at most this many MSMs reduce their buckets RED_J_SMALL per thread
+#ifndef KZGX_SMALL_BATCH_J
+#define KZGX_SMALL_BATCH_J 16
+#endif
 
 template <class C>
 int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
@@ -663,6 +672,41 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   }
   ctx->n_srs = n;
   return fixed_build(ctx, d_canon, n);
+}
+
+// bucket sums + fold (+ affine conversion) of a batch, J buckets per
+// bucket-sum thread
+template <class C, uint32_t NB, uint32_t J>
+static int bucket_reduce(Ctx* ctx, MsmWs& ws, size_t batch, hipStream_t st, uint32_t* d_out, uint32_t* d_out_inf,
+                         uint32_t* xyzz_out) {
+  constexpr uint32_t T1 = NB / J;
+  static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
+  dim3 blk(256);
+  hipLaunchKernelGGL((k_msm_bucket_sums<C, J>), dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
+                     ws.bsum, ws.rt);
+  // workgroup fold (affine conversion inline) for small batches, where four
+  // wavefronts per MSM are what fills the chip; from 256 MSMs the
+  // one-wavefront fold + thread-per-MSM finish is faster (measured, BN254
+  // c = 12: B = 128 wg +2.4%; B = 512 wave +2.8%; B = 2048 wave +6.7%,
+  // profiles/r02_s3_pip_fold_ab.json).  KZGX_PIP_WAVE_FOLD forces the
+  // wavefront form at every batch size (A/B).
+  static const bool fold_wave = std::getenv("KZGX_PIP_WAVE_FOLD") != nullptr;
+  if (T1 % FOLD_WG == 0 && batch < 256 && !fold_wave) {
+    hipLaunchKernelGGL((k_msm_bucket_fold_wg<C, J>), dim3((unsigned)batch), dim3(FOLD_WG), 0, st, ws.rt, T1, xyzz_out,
+                       d_out, d_out_inf);
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
+  }
+  // the fold's XYZZ results go to xyzz_out (chunked callers) or to the
+  // start of bsum, which the fold no longer reads
+  uint32_t* vx = xyzz_out ? xyzz_out : ws.bsum;
+  hipLaunchKernelGGL((k_msm_bucket_fold<C, J>), dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
+                     (uint32_t)batch, vx);
+  if (!xyzz_out)
+    hipLaunchKernelGGL(k_msm_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, vx, (uint32_t)batch,
+                       d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
 }
 
 template <class C, int CB>
@@ -699,7 +743,8 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   // workgroup-crossing partials: ghead / gtail points, gtailk, gflag
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.gpart, batch * nwg * 2 * XB, &ws.gpart_b));
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.gmeta, batch * nwg * 2 * 4, &ws.gmeta_b));
-  KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / RED_J) * 2 * XB, &ws.rt_b));
+  const bool small = batch <= KZGX_SMALL_BATCH_J;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / (small ? RED_J_SMALL : RED_J)) * 2 * XB, &ws.rt_b));
   uint32_t* ghead = ws.gpart;
   uint32_t* gtail = ws.gpart + batch * nwg * xyzz_words<C>();
   uint32_t* gtailk = ws.gmeta;
@@ -733,31 +778,8 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
                        ws.tailk, ws.sstate, (uint32_t)smax, NB, (uint32_t)nwg, ws.bsum, ghead, gtail, gtailk, gflag);
     hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg + 63) / 64), (unsigned)batch), dim3(64), 0, st, NB,
                        (uint32_t)nwg, ghead, gtail, gtailk, gflag, ws.bsum);
-    constexpr uint32_t T1 = NB / RED_J;
-    static_assert(T1 >= 64 && T1 % 64 == 0, "k_msm_bucket_fold: whole (R, T) pairs per lane");
-    hipLaunchKernelGGL(k_msm_bucket_sums<C>, dim3((T1 + 255) / 256, (unsigned)batch), blk, 0, st, ws.offsets, NB,
-                       ws.bsum, ws.rt);
-    // workgroup fold (affine conversion inline) for small batches, where four
-    // wavefronts per MSM are what fills the chip; from 256 MSMs the
-    // one-wavefront fold + thread-per-MSM finish is faster (measured, BN254
-    // c = 12: B = 128 wg +2.4%; B = 512 wave +2.8%; B = 2048 wave +6.7%,
-    // profiles/r02_s3_pip_fold_ab.json).  KZGX_PIP_WAVE_FOLD forces the
-    // wavefront form at every batch size (A/B).
-    static const bool fold_wave = std::getenv("KZGX_PIP_WAVE_FOLD") != nullptr;
-    if (T1 % FOLD_WG == 0 && batch < 256 && !fold_wave) {
-      hipLaunchKernelGGL(k_msm_bucket_fold_wg<C>, dim3((unsigned)batch), dim3(FOLD_WG), 0, st, ws.rt, T1, xyzz_out,
-                         d_out, d_out_inf);
-      KZGX_TRY_HIP(hipGetLastError());
-      return KZGX_OK;
-    }
-    // the fold's XYZZ results go to xyzz_out (chunked callers) or to the
-    // start of bsum, which the fold no longer reads
-    uint32_t* vx = xyzz_out ? xyzz_out : ws.bsum;
-    hipLaunchKernelGGL(k_msm_bucket_fold<C>, dim3((unsigned)((batch + 3) / 4)), blk, 0, st, ws.rt, T1,
-                       (uint32_t)batch, vx);
-    if (!xyzz_out)
-      hipLaunchKernelGGL(k_msm_finish<C>, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, st, vx, (uint32_t)batch,
-                         d_out, d_out_inf);
+    if (small) return bucket_reduce<C, NB, RED_J_SMALL>(ctx, ws, batch, st, d_out, d_out_inf, xyzz_out);
+    return bucket_reduce<C, NB, RED_J>(ctx, ws, batch, st, d_out, d_out_inf, xyzz_out);
   }
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
