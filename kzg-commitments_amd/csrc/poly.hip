@@ -19,6 +19,8 @@
 // needed on the streaming paths.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include <utility>
@@ -58,10 +60,14 @@ KZGX_DEV Fe<FR> wave_prod(Fe<FR> a) {
   return a;
 }
 
+// left-to-right square-and-multiply from the exponent's top set bit (the
+// exponents here are chunk lengths, 3-10 bits: squaring the leading ones
+// would be most of the work on the single-opening latency path)
 template <class FR>
 KZGX_DEV Fe<FR> fe_pow_u32(const Fe<FR>& base_m, uint32_t e) {
-  Fe<FR> acc = fe_one<FR>();
-  for (int b = 31; b >= 0; b--) {
+  if (e == 0) return fe_one<FR>();
+  Fe<FR> acc = base_m;
+  for (int b = 30 - __builtin_clz(e); b >= 0; b--) {
     acc = fe_sqr<FR>(acc);
     if ((e >> b) & 1u) acc = fe_mul<FR>(acc, base_m);
   }
@@ -362,7 +368,14 @@ static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, si
                                 uint32_t* d_q, size_t qstride, uint32_t* d_y, hipStream_t st) {
   if (batch == 0) return KZGX_OK;
   ProfScope prof(ctx, st, "quotient_single");
-  constexpr size_t QBIG_N = 1u << 13;   // from here a single opening spreads over the chip
+  // from QBIG_N coefficients a single opening spreads over the chip: a
+  // degree-4096 create_proof(poly, z, 1) 0.69-0.73 ms with the one-wavefront
+  // kernel, 0.60-0.67 ms chip-wide (profiles/r03_latency_window.json;
+  // KZGX_QBIG_N overrides, for A/B)
+  static const size_t QBIG_N = [] {
+    const char* e = std::getenv("KZGX_QBIG_N");
+    return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)1u << 11;
+  }();
   constexpr size_t QBIG_LANES = 1u << 18;  // 4096 wavefronts: 4 per SIMD
   if (batch <= 4 && n >= QBIG_N) {
     constexpr int N = FR::N;

@@ -30,3 +30,15 @@ for tag in os.environ.get("LAT_TAGS", "pippenger,table").split(","):
         ctx.msm(P)
         ts.append(time.perf_counter() - t0)
     print(tag, "commit median ms %.3f" % (1e3 * float(np.median(ts))), flush=True)
+if os.environ.get("LAT_PROOF"):
+    # single create_proof(poly, z, 1) calls on the Pippenger path (table off)
+    ctx.set_fixed_base(0, 0)
+    zs = np.array([[12345, 0, 0, 0]], dtype=np.uint64)
+    for _ in range(3):
+        ctx.prove_single_batch(P, zs)
+    ts = []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        ctx.prove_single_batch(P, zs)
+        ts.append(time.perf_counter() - t0)
+    print("pippenger proof median ms %.3f" % (1e3 * float(np.median(ts))), flush=True)
