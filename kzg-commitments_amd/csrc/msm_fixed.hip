@@ -460,8 +460,10 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   const size_t n_pad = (n + 63) / 64 * 64;
   if (batch <= 16 && !xyzz_out && n_pad <= 16384 && ft.pts_per_thread == 0 && !lat_off) {
     constexpr int W = FixedWin<C, CB>::W;
-    // G window groups of WG windows: about 128 wavefront partials per MSM
-    int G = (int)std::min<size_t>(W, std::max<size_t>(1, 8192 / n_pad));
+    // G window groups of WG windows: up to 256 wavefront partials per MSM
+    // (degree 4096: 3 groups of 5 windows; one group of 15 made the
+    // accumulation chain 15 additions long)
+    int G = (int)std::min<size_t>(W, std::max<size_t>(1, 16384 / n_pad));
     const int WG = (W + G - 1) / G;
     G = (W + WG - 1) / WG;
     const uint32_t Q = (uint32_t)(n_pad * G / 64);  // <= 256
