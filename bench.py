@@ -96,6 +96,14 @@ def parse():
                     help="skip the throughput-vs-table-size leg (c = 10 .. 16 before the headline table)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-call latency leg (benchmark/benchmark.cpp's timed regions)")
+    ap.add_argument("--no-setup", action="store_true",
+                    help="skip the trusted-setup leg (G1 + G2 SRS of 4097 points, README.md:124)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="cfg2/cfg3/cfg4: weak = --batch per GPU (default); strong = --global-batch split "
+                         "over the ranks")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="--scaling strong: polynomials (openings for cfg3) per step over all ranks "
+                         "(default 8 x the per-GPU default batch)")
     return ap.parse_args()
 
 
@@ -302,11 +310,12 @@ def timed_run(ctx, step, streams, steps, warmup, world, dist, torch, dev):
     ctx.prof_enable(False)
     elapsed = t1 - t0
     kern = {name: ctx.prof_read(name) for name in KERNELS}
+    local_s = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, kern
+    return elapsed, kern, local_s
 
 
 def clock_during(ctx, step, step_s, torch, dev, nsteps=4):
@@ -374,6 +383,117 @@ def mads_per_mixed_add(L):
     return 6 * 2 * L * L + 2 * (L * (L + 1) // 2 + L * L) + 3 * L * L
 
 
+def dist_info(world, dist, torch):
+    """what actually carried the ranks: the process-group backend and, on
+    ROCm, the RCCL version torch was built against (torch.cuda.nccl)"""
+    info = {"world_size": world, "backend": None, "rccl_version": None}
+    if world > 1:
+        try:
+            info["backend"] = str(dist.get_backend())
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            info["backend"] = "unknown (%s)" % e
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001
+        pass
+    return info
+
+
+def rank_records(world, rank, local, dev, local_s, dist, torch, extra=None):
+    """one record per rank: the device it ran on (ordinal, PCI address, UUID,
+    the visible-device mask) and its own elapsed time of the timed region, so
+    a multi-GPU line shows that N distinct GPUs ran and how evenly"""
+    props = torch.cuda.get_device_properties(dev) if dev is not None else None
+    rec = {"rank": rank, "local_rank": local, "device": dev.index if dev is not None else None,
+           "pci": "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                                        getattr(props, "pci_device_id", 0)) if props is not None else None,
+           "uuid": str(getattr(props, "uuid", "")) if props is not None else None,
+           "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES"),
+           "elapsed_s": local_s}
+    if extra:
+        rec.update(extra)
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def accum_kernel_id(curve, c):
+    """SHA-256 of the gfx950 machine code of k_fixed_accum<curve, c> in the
+    loaded libkzgx.so (python/codeobj.py): counter passes are attached to a
+    line only when they measured this exact kernel"""
+    try:
+        import codeobj
+        import kzgx
+        return codeobj.kernel_hash(kzgx.LIB_PATH, *codeobj.fixed_accum_parts(curve, c))
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal
+        return {"sha256": None, "error": str(e)}
+
+
+def matching_traffic(workload, batch, fixed_bits, kernel_sha):
+    """the counter pass (profiles/*pmc_traffic_<workload>*.json, written by
+    scripts/pmc_traffic.py) of this kernel build at this batch and window, or
+    None: a pass of another build is never presented as this kernel's traffic"""
+    import glob
+    if not kernel_sha:
+        return None, None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic_%s*.json" % workload)), reverse=True):
+        try:
+            with open(path) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tj.get("kernel_sha256") == kernel_sha and tj.get("batch") == batch and tj.get("fixed_bits") == fixed_bits:
+            return tj, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def setup_leg(kzgx, curve, K, C, tau, npts=DEGREE + 1, reps=3):
+    """trusted_setup(4097) on the GPU: the G1 and G2 SRS of a degree-4096
+    setup (src/trusted_setup.cpp:21-74; README.md:124 publishes 947.288 ms for
+    the 4096-term G1 + G2 setup on all threads).  A fresh context per run;
+    the first run carries the one-time code-object load and is reported
+    apart.  Checked: every G1 point against the C port, sampled G2 points
+    against the Python oracle's [tau^i]G2."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))  # checker only
+    import corc
+    import pairing_ref as PR
+    times = []
+    g1 = g2 = None
+    for k in range(reps + 1):
+        c2 = kzgx.Context(curve)
+        t0 = time.perf_counter()
+        c2.gen_srs(tau, npts)
+        c2.gen_srs_g2(tau, npts)
+        c2.sync()
+        times.append((time.perf_counter() - t0) * 1e3)
+        if k == reps:
+            g1 = c2.get_srs(npts)
+            g2 = c2.get_srs_g2(npts)
+        c2.close()
+    corc.build()
+    tc = time.perf_counter()
+    ref1 = corc.gen_srs(curve, tau, npts)
+    cpu_g1_ms = (time.perf_counter() - tc) * 1e3
+    w = 4 if curve == "BN254" else 6
+    Q = PR.g2_generator(C)
+    g2_ok = True
+    for i in (0, 1, 2, npts // 2, npts - 2, npts - 1):
+        v = [to_int(g2[i][k * w:(k + 1) * w]) for k in range(4)]
+        g2_ok &= ((v[0], v[1]), (v[2], v[3])) == PR.g2_mul(C, Q, pow(tau, i, C.r))
+    return {"points": npts, "g1_g2_ms": float(np.median(times[1:])), "first_call_ms": times[0],
+            "runs_ms": times[1:],
+            "reference_published_ms": 947.288,
+            "reference_source": "README.md:124, G1 + G2 setup of 4096 terms, all host threads, unstated CPU",
+            "cpu_port_g1_ms": cpu_g1_ms,
+            "cpu_port_note": "G1 half only, C restatement (oracle/kzg_oracle.c: tau^i by repeated products, "
+                             "one double-and-add scalar multiplication per point), 1 thread",
+            "parity": {"g1_points_checked": npts, "g1_ok": bool(np.array_equal(g1, ref1)),
+                       "g2_points_checked": 6, "g2_ok": bool(g2_ok)}}
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -412,7 +532,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
-    if os.environ.get("KZGX_BENCH_LAUNCH_SELFTEST") == "1":
+    selftest = os.environ.get("KZGX_BENCH_LAUNCH_SELFTEST")
+    if selftest == "1":
         # launcher self-test (tests/test_bench_launcher.py, CPU only): report
         # the rank layout and stop before anything touches a device
         fail = os.environ.get("KZGX_BENCH_FAIL_RANK")
@@ -420,6 +541,23 @@ def main():
             return 3
         if rank == 0:
             print(json.dumps({"selftest": True, "world": world, "rank": rank, "gpus": args.gpus}), flush=True)
+        return 0
+    if selftest == "dist":
+        # the per-rank provenance fields of a multi-GPU line, over gloo on
+        # the CPU (no device): every rank's record reaches rank 0
+        import torch
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group(backend="gloo", init_method="env://")
+        t0 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        ranks = rank_records(world, rank, local, None, time.perf_counter() - t0, dist, torch, {"batch": 7 + rank})
+        dinfo = dist_info(world, dist, torch)
+        if rank == 0:
+            print(json.dumps({"selftest": "dist", "ranks": ranks, "dist": dinfo}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
         return 0
     import torch
     import torch.distributed as dist
@@ -454,6 +592,12 @@ def main():
     degree = DEGREE
     n = degree + 1
     B = args.batch or shape["batch"]
+    global_batch = B * world
+    if args.scaling == "strong":
+        # a fixed total batch split over the ranks (the first ranks take the
+        # remainder): 1/2/4/8 GPUs then trace a strong-scaling curve
+        global_batch = args.global_batch or 8 * shape["batch"]
+        B = global_batch // world + (1 if rank < global_batch % world else 0)
     if args.fixed_ppt < 0:
         args.fixed_ppt = shape["points_per_thread"]
     ctx = kzgx.Context(curve, device=local)
@@ -475,6 +619,7 @@ def main():
     step = make_step(ctx, args.workload, n, bufs, streams, S, args.commit_first)
 
     units_per_step = B if args.workload == "cfg3" else 2 * B
+    units_all = global_batch if args.workload == "cfg3" else 2 * global_batch  # every rank's units per step
     # c = 17 cuts BN254's 254-bit scalars to 15 windows (16 at c = 16: +7.8%
     # measured on one box, profiles/r02_ab_table_layout.json); BLS12-381's
     # 255-bit scalars need 16 windows at either width
@@ -484,9 +629,9 @@ def main():
     # kzg::trusted_setup::create_commit / create_proof do without precompute()
     pip = None
     if fixed_bits and not args.no_pippenger:
-        pe, pk = timed_run(ctx, step, streams, max(3, min(args.steps, 6)), 1, world, dist, torch, dev)
+        pe, pk, _ = timed_run(ctx, step, streams, max(3, min(args.steps, 6)), 1, world, dist, torch, dev)
         ps = max(3, min(args.steps, 6))
-        pip = {"value": units_per_step * ps * world / pe, "ms_per_step": pe / ps * 1e3,
+        pip = {"value": units_all * ps / pe, "ms_per_step": pe / ps * 1e3,
                "msm": "pippenger, c=%d, segment %d" % (args.window_bits, args.segment),
                "kernel_ms_per_step": {k: v[0] / ps for k, v in pk.items()}}
     lat = None
@@ -508,10 +653,18 @@ def main():
             tb = time.perf_counter() - tb
             if built != cc:
                 continue
-            ce, _ = timed_run(ctx, step, streams, 4, 1, world, dist, torch, dev)
+            ce, _, _ = timed_run(ctx, step, streams, 4, 1, world, dist, torch, dev)
             curve_pts.append({"window_bits": cc, "gb": ctx.fixed_base_info()[2] / 1e9, "setup_s": tb,
-                              "value": units_per_step * 4 * world / ce})
+                              "value": units_all * 4 / ce})
         ctx.set_fixed_base(0, 0)
+
+    setup = None
+    if rank == 0 and world == 1 and not args.no_setup and args.workload != "cfg3":
+        try:
+            setup = setup_leg(kzgx, curve, K, C, tau)
+        except Exception as e:  # noqa: BLE001 -- a secondary leg, never fatal for the headline
+            setup = {"error": str(e)}
+            print("bench: setup leg failed: %s" % e, file=sys.stderr)
 
     t_setup = time.perf_counter()
     if fixed_bits:
@@ -526,12 +679,14 @@ def main():
     if fb[0]:
         ctx.set_fixed_points_per_thread(args.fixed_ppt)
 
-    elapsed, kern = timed_run(ctx, step, streams, args.steps, args.warmup, world, dist, torch, dev)
+    elapsed, kern, local_s = timed_run(ctx, step, streams, args.steps, args.warmup, world, dist, torch, dev)
 
     # ---- core clock during the step (outside the timed region): a one-wave
     # probe spins on its own stream beside a few more steps (DVFS lowers the
     # clock under this load: profiles/r03_pmc_clock_table_sweep.json) ----
     step_clock = clock_during(ctx, step, elapsed / args.steps, torch, dev)
+    ranks = rank_records(world, rank, local, dev, local_s, dist, torch, {"batch": B})
+    dinfo = dist_info(world, dist, torch)
 
     # ---- parity: every output of the last step (oracle identity, MSM-independent) ----
     checked = ok = 0
@@ -610,27 +765,19 @@ def main():
         # achieved: algorithmic bytes of the step / step time -- never a
         # per-launch duration, which the second stream's launch inflates
         achieved = per_step_bytes / (ms_per_step * 1e-3) / 1e9
-        traffic = None
-
-        def wins_of(c):
-            return (C.r.bit_length() + 1 + c - 1) // c
-
-        tpath = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
-        if os.path.exists(tpath):
-            try:
-                with open(tpath) as f:
-                    tj = json.load(f)
-                entry_b = fb[2] // max(1, wins_of(fb[0]) * fb[1] << (fb[0] - 1)) if fb[0] else 0
-                if tj.get("batch") == B and tj.get("fixed_bits") == fb[0] and tj.get("entry_bytes") == entry_b:
-                    traffic = tj.get("msm_accum_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        total_units = units_per_step * args.steps * world
-        value = total_units / elapsed
         if fb[0]:
             wins = (C.r.bit_length() + 1 + fb[0] - 1) // fb[0]
         else:
             wins = (257 + args.window_bits - 1) // args.window_bits
+        # HBM traffic per launch from a counter pass of THIS kernel build
+        # (code-object hash), batch and window; null otherwise
+        kid = accum_kernel_id(curve, fb[0]) if fb[0] else {"sha256": None}
+        tj, tsrc = matching_traffic(args.workload, B, fb[0], kid.get("sha256"))
+        traffic = tj.get("msm_accum_bytes_per_launch") if tj else None
+        entry_bytes = fb[2] // max(1, wins * fb[1] << (fb[0] - 1)) if fb[0] else 0
+        gathered = B * n * wins * entry_bytes  # table entries looked up per launch (B MSMs)
+        total_units = units_all * args.steps
+        value = total_units / elapsed
         madds = (B * n + (0 if args.workload == "cfg3" else B * n)) * wins
         madd_rate = madds / (ms_per_step * 1e-3)
         peak = None
@@ -660,7 +807,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             # 0.905 commits/s + 0.925 proofs/s (README.md:132) -> 2 units per 2.185 s
             "vs_baseline": (value / (2.0 / (REF_COMMIT_S + REF_PROOF_S))) if args.workload == "cfg2" else None,
             "dtype": "u32 (radix-2^29 Montgomery limbs, %d-bit Fp)" % (254 if curve == "BN254" else 381),
@@ -672,6 +819,7 @@ def main():
                 "curve": curve,
                 "degree": degree,
                 "batch_per_gpu": B,
+                "global_batch": global_batch,
                 "srs_points": 5000,
                 "parallelism": "dp%d (independent batches, no collective)" % world,
                 "msm": ("fixed-base table, c=%d, %d windows, %.1f GB, %d points/thread" % (
@@ -687,25 +835,32 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": tsrc,
+                "traffic_over_algorithmic": traffic / bytes_per_launch if traffic else None,
+                "traffic_over_gathered_entries": traffic / gathered if traffic and gathered else None,
+                "gathered_entry_bytes_per_launch": gathered or None,
+                "kernel_code": kid,
                 "algorithmic_bytes_per_step": per_step_bytes,
                 "launches_per_step": launches_per_step,
                 "avg_launch_ms": avg_launch_ms,
                 "achieved_from": "algorithmic bytes per step / ms_per_step" + (
                     " (the commit and proof launches overlap on two streams, so avg_launch_ms is not an isolated "
                     "duration; profiles/*serial* hold the one-stream rocprof run)" if overlapped else ""),
-                "note": "integer-VALU bound (no MFMA); see secondary.valu_roofline",
+                "note": "integer-VALU bound (no MFMA); see secondary.mad_issue",
             },
             "secondary": {
                 "mixed_adds_per_s": madd_rate,
                 "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
                 "fixed_table_setup_s": t_setup if fb[0] else None,
                 "fixed_table_bytes": fb[2] if fb[0] else None,
-                "valu_roofline": None if not peak else {
+                "valu_yardstick": None if not peak else {
                     "achieved_mixed_adds_per_s": madd_rate,
-                    "peak_mixed_adds_per_s": peak,
-                    "frac": madd_rate / peak,
-                    "peak_from": "kzgx_microbench_mixed_add: the accumulation loop's XYZZ mixed add on "
-                                 "register-resident operands at the kernel's occupancy, whole GPU, measured live",
+                    "yardstick_mixed_adds_per_s": peak,
+                    "ratio": madd_rate / peak,
+                    "from": "kzgx_microbench_mixed_add: the accumulation loop's XYZZ mixed add on "
+                            "register-resident operands at one occupancy, whole GPU, measured live. A yardstick "
+                            "of the instruction mix, not a ceiling (BLS12-381 exceeds it): mad_issue is the "
+                            "hardware-anchored figure",
                 },
                 "mad_issue": None if not mad_peak else {
                     "mads_per_mixed_add": mpa,
@@ -728,6 +883,9 @@ def main():
                 "table_curve": curve_pts,
                 "pippenger": pip,
                 "latency": lat,
+                "setup_ms": setup,
+                "ranks": ranks,
+                "dist": dinfo,
             },
             "parity": {"checked": checked, "ok": int(ok), "first_failure": bad,
                        "method": "every output of the last step: commit = [P(tau)]G1, proof = [q(tau)]G1, "
@@ -798,24 +956,57 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                           stream.cuda_stream)
         return torch.cat([d_res, d_res_inf.to(torch.int64)])
 
+    # per-phase HIP events on the step's stream: start, partial MSM enqueued,
+    # all-gather done (the collective's completion is ordered before the
+    # stream's next work), fold done
+    marks = []
+    timing = [False]
+
+    def mark(_phase):
+        if timing[0]:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            marks[-1].append(e)
+
     def step():
+        if timing[0]:
+            marks.append([])
+            mark("start")
         with torch.cuda.stream(stream):
-            return kzgx_dist.sharded_commit_tensor(n, world, rank, w64, partial, fold, dist, torch)
+            return kzgx_dist.sharded_commit_tensor(n, world, rank, w64, partial, fold, dist, torch, on_phase=mark)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    timing[0] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    timing[0] = False
+    local_s = elapsed
+    # phase times of this rank, mean over the timed steps
+    names = ["partial_msm", "all_gather", "fold"]
+    phase_tot = [0.0] * 3
+    for m in marks:
+        for k in range(min(3, len(m) - 1)):
+            phase_tot[k] += m[k].elapsed_time(m[k + 1])
+    my_phases = {names[k]: phase_tot[k] / max(1, len(marks)) for k in range(3 if world > 1 else 1)}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    ranks = rank_records(world, rank, local, dev, local_s, dist, torch,
+                         {"shard_points": count, "phase_ms_per_step": my_phases})
+    dinfo = dist_info(world, dist, torch)
+    phases = {"rank0": my_phases,
+              "max_over_ranks": {k: max(r["phase_ms_per_step"].get(k, 0.0) for r in ranks) for k in my_phases},
+              "from": "HIP events on the step stream: partial_msm = this rank's shard MSM; all_gather = the "
+                      "RCCL all-gather of the packed partial points (until the stream may use them); fold = "
+                      "kzgx_g1_sum_device of the gathered points"}
     if rank == 0:
         xys, infs = kzgx_dist.unpack_points(res.cpu().numpy(), w64)
         xy, inf = xys[0], bool(infs[0])
@@ -887,16 +1078,20 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                 "traffic": None,
                 "algorithmic_bytes_per_step": unit_bytes,
                 "achieved_from": "algorithmic bytes of one commit / ms_per_step",
-                "note": "integer-VALU bound (no MFMA); see secondary.valu_roofline",
+                "note": "integer-VALU bound (no MFMA); see secondary.valu_yardstick",
             },
             "secondary": {
                 "fixed_table_setup_s": t_setup,
-                "valu_roofline": None if not peak else {
+                "valu_yardstick": None if not peak else {
                     "achieved_mixed_adds_per_s": madd_rate,
-                    "peak_mixed_adds_per_s": peak,
-                    "frac": madd_rate / peak,
-                    "peak_from": "kzgx_microbench_mixed_add on rank 0's GPU x ranks, measured live",
+                    "yardstick_mixed_adds_per_s": peak,
+                    "ratio": madd_rate / peak,
+                    "from": "kzgx_microbench_mixed_add on rank 0's GPU x ranks, measured live (a yardstick of "
+                            "the instruction mix, not a ceiling)",
                 },
+                "phase_ms_per_step": phases,
+                "ranks": ranks,
+                "dist": dinfo,
             },
             "parity": {"checked": 1, "ok": int(ok), "method": "[P(tau)]G1 identity"},
             "cpu_baseline": cpu,

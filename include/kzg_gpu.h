@@ -117,8 +117,10 @@ int kzgx_fixed_base_bytes(int curve, int c, size_t n_points, size_t* bytes);
  * table over n_points fits budget_bytes AND the device's free memory
  * (less a 4 GiB margin for workspaces); builds it (as kzgx_set_fixed_base)
  * and returns it in *c_out, or installs no table (*c_out = 0: every MSM on
- * Pippenger) when even c = 7 does not fit.  Extension with no reference
- * counterpart: trusted_setup::precompute_budget. */
+ * Pippenger) when even c = 7 does not fit.  n_points is clamped to the
+ * installed SRS; KZGX_ERR_NO_SRS before one is loaded (the free-memory
+ * check needs the SRS and its window tables in place).  Extension with no
+ * reference counterpart: trusted_setup::precompute_budget. */
 int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_points, int* c_out);
 /* SRS points summed per accumulation thread on the fixed-base path
  * (0 = automatic, the default: 16 for batches of >= 64 MSMs, else enough

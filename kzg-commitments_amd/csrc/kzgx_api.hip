@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "curve_consts.h"
 #include "kzgx_internal.hpp"
 
 struct kzgx_ctx {
@@ -87,6 +88,28 @@ int stage(kzgx_ctx* ctx, int slot, size_t bytes, void** out) {
 
 size_t point_words(const kzgx_ctx* ctx) { return 2 * (size_t)ctx->c.base_words(); }
 
+// x mod r for a 4 x 64-bit little-endian value: the reference converts its
+// evaluation points into ZZ_p (src/trusted_setup.cpp:214-219), so x and x + r
+// are the same point.  Argument normalisation only (a handful of compares and
+// subtractions per point), done before the repeated-point check.
+template <class FR>
+std::array<uint64_t, 4> fr_reduce(const uint64_t* x) {
+  uint64_t r[4], v[4] = {x[0], x[1], x[2], x[3]};
+  for (int i = 0; i < 4; i++) r[i] = (uint64_t)FR::P[2 * i] | ((uint64_t)FR::P[2 * i + 1] << 32);
+  for (;;) {
+    int i = 3;
+    while (i >= 0 && v[i] == r[i]) i--;
+    if (i >= 0 && v[i] < r[i]) break;  // v < r (i < 0: v == r, reduces to 0)
+    unsigned __int128 borrow = 0;
+    for (int k = 0; k < 4; k++) {
+      const unsigned __int128 d = (unsigned __int128)v[k] - r[k] - borrow;
+      v[k] = (uint64_t)d;
+      borrow = (d >> 64) & 1;
+    }
+  }
+  return {v[0], v[1], v[2], v[3]};
+}
+
 }  // namespace
 
 extern "C" {
@@ -154,6 +177,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
                   w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig};
     for (void* p : wb)
       if (p) (void)hipFree(p);
+    if (w.done) (void)hipEventDestroy(w.done);
   }
   (void)hipStreamDestroy(c.stream);
   delete ctx;
@@ -276,6 +300,10 @@ int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_poin
   KZGX_TRY(activate(ctx));
   if (!c_out || n_points == 0) return KZGX_ERR_ARG;
   *c_out = 0;
+  // the budget is sized against the free HBM after the SRS and its window
+  // tables exist, and for the points that will actually be tabled
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  if (n_points > ctx->c.n_srs) n_points = ctx->c.n_srs;
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
   kzgx::fixed_free(&ctx->c);  // the old table's memory counts as free
   size_t free_b = 0, total_b = 0;
@@ -290,7 +318,11 @@ int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_poin
       *c_out = c;
       return KZGX_OK;
     }
-    if (rc != KZGX_ERR_OOM) return rc;
+    if (rc != KZGX_ERR_OOM) {
+      ctx->c.fixed.c_req = 0;  // no half-requested window left for the next SRS upload
+      ctx->c.fixed.n_req = 0;
+      return rc;
+    }
   }
   ctx->c.fixed.c_req = 0;
   ctx->c.fixed.n_req = 0;
@@ -462,7 +494,7 @@ int kzgx_prove_single_batch_device(kzgx_ctx* ctx, const void* d_coeffs, size_t n
   const size_t nq = n > 0 ? n - 1 : 0;
   if (nq > ctx->c.n_srs) return KZGX_ERR_DEGREE;
   hipStream_t st = pick(ctx, stream);
-  kzgx::MsmWs* ws = ctx->c.ws_for(st);
+  kzgx::WsLease ws = ctx->c.ws_for(st);
   if (!ws) return KZGX_ERR_ARG;
   void* d_q = nullptr;
   if (nq) {
@@ -481,23 +513,30 @@ int kzgx_prove_range(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, const uint
   while (n > 0 && (coeffs[4 * (n - 1)] | coeffs[4 * (n - 1) + 1] | coeffs[4 * (n - 1) + 2] | coeffs[4 * (n - 1) + 3]) == 0)
     n--;  // NTL keeps polynomials normalized
   if (n > len && n - len > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  // the points as residues mod r (x and x + r are one point, as in ZZ_p)
+  std::vector<uint64_t> xr(4 * len);
+  for (size_t i = 0; i < len; i++) {
+    const auto v = ctx->c.curve == KZGX_CURVE_BN254 ? fr_reduce<kzgx::BN254Fr>(xs + 4 * i)
+                                                    : fr_reduce<kzgx::BLS12381Fr>(xs + 4 * i);
+    std::copy(v.begin(), v.end(), xr.begin() + 4 * i);
+  }
   {
     // repeated points: the reference's interpolation (NTL polyfit) fails on
     // them, so does this call (P div Z alone would still be defined)
     std::vector<std::array<uint64_t, 4>> sorted(len);
-    for (size_t i = 0; i < len; i++) sorted[i] = {xs[4 * i + 3], xs[4 * i + 2], xs[4 * i + 1], xs[4 * i]};
+    for (size_t i = 0; i < len; i++) sorted[i] = {xr[4 * i + 3], xr[4 * i + 2], xr[4 * i + 1], xr[4 * i]};
     std::sort(sorted.begin(), sorted.end());
     if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) return KZGX_ERR_DIV_ZERO;
   }
   hipStream_t st = ctx->c.stream;
-  kzgx::MsmWs* ws = ctx->c.ws_for(st);
+  kzgx::WsLease ws = ctx->c.ws_for(st);
   if (!ws) return KZGX_ERR_ARG;
   void *d_c = nullptr, *d_x, *d_o;
   if (n) KZGX_TRY(stage(ctx, 0, n * 32, &d_c));
   KZGX_TRY(stage(ctx, 1, len * 32, &d_x));
   KZGX_TRY(stage(ctx, 2, point_words(ctx) * 4 + 16, &d_o));
   if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, n * 32, hipMemcpyHostToDevice, st));
-  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xs, len * 32, hipMemcpyHostToDevice, st));
+  KZGX_TRY_HIP(hipMemcpyAsync(d_x, xr.data(), len * 32, hipMemcpyHostToDevice, st));
   size_t nq = 0;
   if (n > len) {
     KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ws->q, (n - len) * 32, &ws->q_b));
@@ -980,6 +1019,7 @@ extern "C" int kzgx_debug_ws_read(kzgx_ctx* ctx, const char* name, void* host, s
   else if (s == "cursors") src = w->cursors, cap = w->cursors_b;
   else if (s == "gmeta") src = w->gmeta, cap = w->gmeta_b;
   else if (s == "gpart") src = w->gpart, cap = w->gpart_b;
+  else if (s == "q") src = w->q, cap = w->q_b;
   if (!src || bytes > cap) return KZGX_ERR_ARG;
   KZGX_TRY_HIP(hipDeviceSynchronize());
   KZGX_TRY_HIP(hipMemcpy(host, src, bytes, hipMemcpyDeviceToHost));

@@ -46,6 +46,30 @@ struct MsmWs {
   hipStream_t owner = nullptr;  // workspaces are per stream so calls on
   bool used = false;            // different streams may run concurrently
   uint64_t bound_at = 0;        // Ctx::ws_clock when bound to owner
+  hipEvent_t done = nullptr;    // recorded on the owner stream after the last call that used this slot
+  bool done_recorded = false;
+};
+
+struct Ctx;
+// A workspace bound to a stream for the length of one call.  Its destructor
+// records the slot's `done` event on that stream after everything the call
+// enqueued, so rebinding the slot later waits on the event -- never on the
+// old owner stream's handle, which the caller may have destroyed since.
+class WsLease {
+ public:
+  WsLease(Ctx* c, MsmWs* w, hipStream_t st) : c_(c), w_(w), st_(st) {}
+  WsLease(const WsLease&) = delete;
+  WsLease& operator=(const WsLease&) = delete;
+  ~WsLease();
+  MsmWs* operator->() const { return w_; }
+  MsmWs& operator*() const { return *w_; }
+  bool operator!() const { return w_ == nullptr; }
+  MsmWs* get() const { return w_; }
+
+ private:
+  Ctx* c_;
+  MsmWs* w_;
+  hipStream_t st_;
 };
 
 constexpr int KZGX_MAX_STREAMS = 8;
@@ -99,35 +123,47 @@ struct Ctx {
   FixedTable fixed;
   // the workspace bound to stream st (claimed on first use; every lookup
   // refreshes its use stamp).  With more than KZGX_MAX_STREAMS distinct
-  // streams the least recently USED slot is rebound after its previous
-  // owner stream has drained (hipStreamSynchronize of that stream only:
-  // other streams and contexts keep running; a stream must outlive the
-  // calls made on it); nullptr only if that synchronisation fails.
+  // streams the least recently USED slot is rebound once the work of its
+  // last call has drained: hipEventSynchronize of the slot's own event,
+  // recorded by the lease after that call's last enqueue (other streams and
+  // contexts keep running, and the old owner stream may already be
+  // destroyed).  A null lease only if that synchronisation fails.
   uint64_t ws_clock = 0;
   MsmWs* ws_find(hipStream_t st) {
     for (auto& w : ws)
       if (w.used && w.owner == st) return &w;
     return nullptr;
   }
-  MsmWs* ws_for(hipStream_t st) {
+  WsLease ws_for(hipStream_t st) {
     if (MsmWs* w = ws_find(st)) {
       w->bound_at = ++ws_clock;
-      return w;
+      return WsLease(this, w, st);
     }
     for (auto& w : ws)
       if (!w.used) {
         w.used = true;
         w.owner = st;
         w.bound_at = ++ws_clock;
-        return &w;
+        return WsLease(this, &w, st);
       }
     MsmWs* lru = &ws[0];
     for (auto& w : ws)
       if (w.bound_at < lru->bound_at) lru = &w;
-    if (hipStreamSynchronize(lru->owner) != hipSuccess) return nullptr;
+    if (lru->done_recorded && hipEventSynchronize(lru->done) != hipSuccess) return WsLease(this, nullptr, st);
+    lru->done_recorded = false;
     lru->owner = st;
     lru->bound_at = ++ws_clock;
-    return lru;
+    return WsLease(this, lru, st);
+  }
+  // end of a call's use of w on st (WsLease destructor)
+  void ws_release(MsmWs* w, hipStream_t st) {
+    if (!w->done && hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
+      w->done = nullptr;
+      (void)hipStreamSynchronize(st);  // no event: drain now, while st is known to be alive
+      return;
+    }
+    w->done_recorded = hipEventRecord(w->done, st) == hipSuccess;
+    if (!w->done_recorded) (void)hipStreamSynchronize(st);
   }
   bool prof_on = false;
   std::vector<ProfRec> prof;
@@ -142,6 +178,10 @@ struct Ctx {
   size_t stage_b[4] = {0, 0, 0, 0};
   int base_words() const { return curve == KZGX_CURVE_BN254 ? 8 : 12; }
 };
+
+inline WsLease::~WsLease() {
+  if (w_) c_->ws_release(w_, st_);
+}
 
 // bracket one launch with events when profiling is enabled
 struct ProfScope {

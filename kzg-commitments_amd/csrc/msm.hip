@@ -726,7 +726,7 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   const size_t nblk = (n + SORT_BLK - 1) / SORT_BLK;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
   if (batch > 65535 || nblk > 65535 || nwg > 65535) return KZGX_ERR_ARG;  // grid limits
-  MsmWs* wsp = ctx->ws_for(st);
+  WsLease wsp = ctx->ws_for(st);
   if (!wsp) return KZGX_ERR_ARG;  // workspace binding failed (device sync error)
   MsmWs& ws = *wsp;
   // counts: per-(MSM, count block) histograms; cursors: their write bases;
@@ -826,7 +826,7 @@ static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uin
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
   const size_t full = n / MSM_CHUNK, rest = n % MSM_CHUNK;
   const size_t parts = full + (rest ? 1 : 0);
-  MsmWs* ws = ctx->ws_for(st);
+  WsLease ws = ctx->ws_for(st);
   if (!ws) return KZGX_ERR_ARG;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws->parts, parts * XB, &ws->parts_b));
   uint32_t* parts_buf = ws->parts;

@@ -339,9 +339,11 @@ constexpr uint32_t FIXED_J = 16;  // multiples per table-build thread
 #define KZGX_FIXED_PM_MAX_C 12
 #endif
 static bool fixed_point_major(int c, int layout_req) {
+  // an explicit kzgx_set_fixed_base_layout(0/1) wins; the environment knob
+  // (A/B runs) only overrides the automatic choice
+  if (layout_req >= 0) return layout_req != 0;
   static const char* e = std::getenv("KZGX_FIXED_POINT_MAJOR");
   if (e && *e) return std::atoi(e) != 0;
-  if (layout_req >= 0) return layout_req != 0;
   return c <= KZGX_FIXED_PM_MAX_C;
 }
 
@@ -467,7 +469,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
     const int WG = (W + G - 1) / G;
     G = (W + WG - 1) / WG;
     const uint32_t Q = (uint32_t)(n_pad * G / 64);  // <= 256
-    MsmWs* wsp = ctx->ws_for(st);
+    WsLease wsp = ctx->ws_for(st);
     if (!wsp) return KZGX_ERR_ARG;
     KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
     ProfScope p(ctx, st, "msm_accum");
@@ -497,7 +499,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
       static const size_t tmult = std::getenv("KZGX_FLAT_TMULT") ? std::strtoul(std::getenv("KZGX_FLAT_TMULT"), nullptr, 10) : 1;
       const uint32_t T = (uint32_t)std::max<size_t>(4096, kSlots * (tmult ? tmult : 1) / batch / 4096 * 4096);
       const uint32_t Q = (uint32_t)((terms + T - 1) / T);
-      MsmWs* wsp = ctx->ws_for(st);
+      WsLease wsp = ctx->ws_for(st);
       if (!wsp) return KZGX_ERR_ARG;
       MsmWs& ws = *wsp;
       KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * (T / 64) * XB, &ws.fpart_b));
@@ -532,7 +534,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   // level.
   const bool wave_red = batch <= 16 && T > 1024 && !xyzz_out;
   if (wave_red && T > 64 * 128) T = (T + 4095) / 4096 * 4096;
-  MsmWs* wsp = ctx->ws_for(st);
+  WsLease wsp = ctx->ws_for(st);
   if (!wsp) return KZGX_ERR_ARG;
   MsmWs& ws = *wsp;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * T * XB, &ws.fpart_b));

@@ -383,7 +383,7 @@ static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, si
     const size_t T = (n + L - 1) / L;
     const size_t Tw = (T + 255) / 256 * 256;  // whole workgroups
     const size_t G = Tw / 64;
-    MsmWs* ws = ctx->ws_for(st);
+    WsLease ws = ctx->ws_for(st);
     if (!ws) return KZGX_ERR_ARG;
     KZGX_TRY(dev_alloc(ctx, (void**)&ws->qbig, (Tw + 2 * G) * N * sizeof(uint32_t), &ws->qbig_b));
     uint32_t* cl = ws->qbig;
@@ -614,13 +614,15 @@ static int prove_range_poly_impl(Ctx* ctx, const uint32_t* d_P, size_t n, const 
   if (n <= len) return KZGX_OK;  // deg P < len: I = P, q = 0 (NTL normalizes to the zero polynomial)
   const size_t m = n - len;
   if (prove_range_by_division<FR>(n, len)) {
-    // ping-pong between d_q and a scratch buffer, ending in d_q
-    KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, (n - 1) * eb, &ctx->poly_ws2_b));
-    uint32_t* tmp = (uint32_t*)ctx->d_poly_ws2;
+    // Intermediate quotients ping-pong between two scratch halves of n - 1
+    // coefficients each; only the last division (m coefficients) writes d_q,
+    // which the caller sizes for exactly m.
+    KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws2, 2 * (n - 1) * eb, &ctx->poly_ws2_b));
+    uint32_t* half[2] = {(uint32_t*)ctx->d_poly_ws2, (uint32_t*)ctx->d_poly_ws2 + (n - 1) * N};
     const uint32_t* cur = d_P;
     size_t ncur = n;
     for (size_t i = 0; i < len; i++) {
-      uint32_t* dst = ((len - 1 - i) & 1) ? tmp : d_q;
+      uint32_t* dst = i + 1 == len ? d_q : half[i & 1];
       KZGX_TRY(quotient_single_impl<FR>(ctx, cur, ncur, 0, d_x + i * N, 1, dst, 0, nullptr, st));
       cur = dst;
       ncur--;

@@ -171,6 +171,17 @@ class Context:
         _chk(lib().kzgx_create(ctypes.byref(h), CURVES[curve], device), "kzgx_create")
         self.h = h
 
+    def debug_ws_read(self, name: str, nbytes: int) -> np.ndarray:
+        """bytes of one workspace buffer of the context stream (test hook:
+        kzgx_debug_ws_read, declared outside kzg_gpu.h)"""
+        L = lib()
+        fn = L.kzgx_debug_ws_read
+        fn.restype = ctypes.c_int
+        fn.argtypes = [vp, ctypes.c_char_p, vp, sz]
+        a = np.zeros(nbytes, dtype=np.uint8)
+        _chk(fn(self.h, name.encode(), a.ctypes.data, nbytes), "kzgx_debug_ws_read")
+        return a
+
     def close(self):
         if getattr(self, "h", None):
             lib().kzgx_destroy(self.h)

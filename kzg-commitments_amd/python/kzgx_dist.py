@@ -64,7 +64,7 @@ def sharded_commit(n: int, world: int, rank: int, w64: int,
 def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
                           partial_msm: Callable[[int, int], "object"],
                           fold: Callable[["object", "object"], "object"],
-                          dist, torch) -> "object":
+                          dist, torch, on_phase: Optional[Callable[[str], None]] = None) -> "object":
     """Device-resident form of sharded_commit (bench.py's configs[4] step).
 
     partial_msm(start, count) -> this rank's packed partial (2 W64 + 1 int64:
@@ -72,15 +72,22 @@ def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
     no host synchronisation; the packed partials are all-gathered (RCCL over
     xGMI on GPU, gloo on CPU) straight into device tensors; fold(points
     (world, 2 W64) int64, flags (world,) int32) -> packed result tensor.
-    Nothing crosses to the host inside a step."""
+    Nothing crosses to the host inside a step.  on_phase(name), if given, is
+    called after each phase is enqueued ("partial", "gather", "fold"), e.g.
+    to record timing events on the step's stream."""
+    mark = on_phase or (lambda _name: None)
     start, count = shard_range(n, world, rank)
     packed = partial_msm(start, count)
+    mark("partial")
     if world == 1:
         return packed
     outs = [torch.empty_like(packed) for _ in range(world)]
     dist.all_gather(outs, packed)
     g = torch.stack(outs)
-    return fold(g[:, : 2 * w64].contiguous(), g[:, 2 * w64].to(torch.int32).contiguous())
+    mark("gather")
+    res = fold(g[:, : 2 * w64].contiguous(), g[:, 2 * w64].to(torch.int32).contiguous())
+    mark("fold")
+    return res
 
 
 def torch_all_gather(dist, device: Optional[object] = None):

@@ -46,3 +46,18 @@ def test_world_must_match_gpus():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "4"], env=env, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_rank_records_reach_rank0():
+    """every rank's provenance record (rank, device, elapsed, its own fields)
+    and the backend in use appear on rank 0's line (a SCALE run
+    must show what ran); gloo on the CPU here, RCCL on the GPU node"""
+    r = _run(3, {"KZGX_BENCH_LAUNCH_SELFTEST": "dist"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    ranks = lines[0]["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1, 2]
+    assert [x["batch"] for x in ranks] == [7, 8, 9]
+    assert all(x["elapsed_s"] >= 0 for x in ranks)
+    assert lines[0]["dist"]["backend"] == "gloo" and lines[0]["dist"]["world_size"] == 3
