@@ -12,6 +12,8 @@
 #   bench[:ARGS]      python bench.py ARGS (commas -> spaces)
 #   prof[:ARGS]       rocprofv3 --kernel-trace --stats around bench.py ARGS
 #   pmc:CTRS[:ARGS]   one rocprofv3 --pmc pass (CTRS comma-separated) around bench.py ARGS
+#   py:SCRIPT[,ARGS]  python3 scripts/SCRIPT ARGS
+#   profpy:SCRIPT[,ARGS] rocprofv3 --kernel-trace --stats around python3 scripts/SCRIPT ARGS
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 TAG=$1
@@ -62,6 +64,21 @@ for st in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } -d "$OUT/pmc_$n" -o pmc --output-format csv \
         -- python3 -u bench.py ${bargs//,/ } > "$OUT/pmc_$n.json" 2> "$OUT/pmc_$n.err" \
         || { tail -20 "$OUT/pmc_$n.err"; exit 1; }
+      ;;
+    py)
+      # py:SCRIPT[,ARGS] -- a script under scripts/ (commas -> spaces)
+      set -- ${arg//,/ }
+      timeout -k 10 600 python3 -u "scripts/$1" "${@:2}" > "$OUT/py_$n.txt" 2>&1 \
+        || { tail -20 "$OUT/py_$n.txt"; exit 1; }
+      tail -20 "$OUT/py_$n.txt"
+      ;;
+    profpy)
+      # profpy:SCRIPT[,ARGS] -- rocprofv3 kernel trace + stats around a script under scripts/
+      set -- ${arg//,/ }
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/profpy_$n" -o prof --output-format csv \
+        -- python3 -u "scripts/$1" "${@:2}" > "$OUT/profpy_$n.txt" 2>&1 \
+        || { tail -20 "$OUT/profpy_$n.txt"; exit 1; }
+      tail -12 "$OUT/profpy_$n.txt"
       ;;
     *)
       echo "unknown step $st"
