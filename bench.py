@@ -136,9 +136,10 @@ def random_fr(rng, shape, r):
 
 def fixed_table_bytes(curve, c, npts):
     """device bytes of the fixed-base table (msm_fixed.hip: W x n x 2^(c-1)
-    entries of 64 B (BN254, packed words) / 112 B (BLS12-381, radix-2^29 limbs))"""
+    entries of 64 B (BN254, packed words) / 112 B (BLS12-381, radix-2^29 limbs);
+    W = ceil(bits(r) / c) regular odd digits, fixed_accum.hpp)"""
     bits = 254 if curve == "BN254" else 255
-    w = (bits + 1 + c - 1) // c
+    w = (bits + c - 1) // c
     return w * npts * (1 << (c - 1)) * (64 if curve == "BN254" else 112)
 
 
@@ -766,7 +767,7 @@ def main():
         # per-launch duration, which the second stream's launch inflates
         achieved = per_step_bytes / (ms_per_step * 1e-3) / 1e9
         if fb[0]:
-            wins = (C.r.bit_length() + 1 + fb[0] - 1) // fb[0]
+            wins = (C.r.bit_length() + fb[0] - 1) // fb[0]  # regular odd digits
         else:
             wins = (257 + args.window_bits - 1) // args.window_bits
         # HBM traffic per launch from a counter pass of THIS kernel build
@@ -1020,7 +1021,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         P_b = 2 * w64 * 8
         unit_bytes = n * (P_b + 32) + P_b
         achieved = unit_bytes / (ms_per_step * 1e-3) / 1e9
-        wins = ((C.r.bit_length() + 1 + fixed_bits - 1) // fixed_bits) if fixed_bits else \
+        wins = ((C.r.bit_length() + fixed_bits - 1) // fixed_bits) if fixed_bits else \
             (257 + args.window_bits - 1) // args.window_bits
         madd_rate = n * wins / (ms_per_step * 1e-3)  # all ranks' mixed additions per second
         peak = None

@@ -46,12 +46,12 @@ struct TabStrides {
 
 template <class C, int CB>
 struct FixedWin {
-  // signed digits of a scalar < r need W c >= bits(r) + 1: the top digit
-  // then absorbs the final carry without overflowing H
-  static constexpr int W = (C::SCALAR_BITS + 1 + CB - 1) / CB;
+  // regular odd digits (below) of a scalar k < r < 2^SCALAR_BITS need
+  // W c >= SCALAR_BITS: the top digit 2 (u >> c (W - 1)) + 1, u = k >> 1 <
+  // 2^(SCALAR_BITS - 1), then indexes one of the H table entries
+  static constexpr int W = (C::SCALAR_BITS + CB - 1) / CB;
   static constexpr uint32_t H = 1u << (CB - 1);
 };
-
 
 template <class C>
 KZGX_DEV Affine<C> packed_load(const uint32_t* __restrict__ p) {
@@ -122,13 +122,47 @@ KZGX_DEV void shr_scalar(uint32_t (&s)[8]) {
   s[7] >>= CB;
 }
 
-// next signed digit from the low CB bits of s (consumed), carry in/out
+// Regular odd signed digits (Joye-Tunstall "regular recoding").  For an odd
+// k with u = k >> 1:
+//   d_w = 2 ((u >> c w) mod 2^c) + 1 - 2^c   (w < W - 1),
+//   d_{W-1} = 2 (u >> c (W - 1)) + 1,
+// sum_w d_w 2^(c w) = k, and every digit is odd: never zero.  The table then
+// holds the odd multiples M[w][i][j] = (2 j + 1) 2^(c w) P_i, j = (|d| - 1) / 2
+// < H, and every term is one mixed addition -- no zero-digit branch, whose
+// accumulator merge cost ~36 register copies per term.  An even k is
+// replaced by r - k (odd; r is odd) with every digit negated:
+// (r - k) P = -k P for P of order r.  k = 0 becomes r: its terms sum to O
+// through exact additions.  Digit w reads bits [c w, c w + c) of u alone
+// (no carry), so a thread may start at any window.
+//
+// odd_prepare: canonical s (scalar_reduce first) -> u = k' >> 1 in s, and the
+// sign flip (1 when k was even)
+template <class C>
+KZGX_DEV uint32_t odd_prepare(uint32_t (&s)[8]) {
+  using R = typename C::Fr;
+  const uint32_t flip = (s[0] & 1u) ^ 1u;
+  // s = flip ? r - s : s, branch-free (r - s >= 0 for canonical s)
+  const uint32_t m = 0u - flip;
+  int64_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int64_t v = (int64_t)(R::P[k] & m) - (int64_t)(s[k] & m) + (int64_t)(s[k] & ~m) + br;
+    s[k] = (uint32_t)v;
+    br = v >> 32;
+  }
+  shr_scalar<1>(s);
+  return flip;
+}
+
+// table entry index j and sign of the digit whose window bits are the low CB
+// bits of s (top: the remaining bits, top digit of the scalar)
 template <int CB>
-KZGX_DEV int next_digit(uint32_t (&s)[8], uint32_t& carry) {
-  uint32_t raw = (s[0] & ((1u << CB) - 1u)) + carry;
-  shr_scalar<CB>(s);
-  carry = raw > (1u << (CB - 1)) ? 1u : 0u;
-  return (int)raw - (int)(carry << CB);
+KZGX_DEV void odd_digit(uint32_t s0, bool top, uint32_t flip, uint32_t& j, uint32_t& neg) {
+  constexpr uint32_t H = 1u << (CB - 1);
+  const uint32_t m = s0 & ((1u << CB) - 1u);
+  const uint32_t hi = m >> (CB - 1);  // 1: d > 0
+  j = top ? s0 : ((m ^ (hi - 1u)) & (H - 1u));
+  neg = (top ? 0u : hi ^ 1u) ^ flip;
 }
 
 // thread t of MSM b sums the W digit terms of points i = t, t + T, t + 2T, ...
@@ -189,9 +223,6 @@ constexpr int fixed_accum_waves() {
   return C::Fp29::L <= 9 ? KZGX_FIXED_WAVES_BN : KZGX_FIXED_WAVES_BLS;
 }
 
-typedef __attribute__((address_space(1))) const void* kzgx_gptr_t;
-typedef __attribute__((address_space(3))) void* kzgx_lptr_t;
-
 KZGX_DEV void scalar_load(const uint32_t* __restrict__ src, uint32_t (&s)[8]) {
   const uint4 lo = reinterpret_cast<const uint4*>(src)[0];
   const uint4 hi = reinterpret_cast<const uint4*>(src)[1];
@@ -199,146 +230,111 @@ KZGX_DEV void scalar_load(const uint32_t* __restrict__ src, uint32_t (&s)[8]) {
   s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
 }
 
-// The digit terms of one accumulation thread, in order: points i = t,
-// t + T, t + 2T, ... (a wavefront reads 64 consecutive scalars per point
-// step), windows w = 0 .. W - 1 of each.  next() recodes the next signed
-// digit (0: no addition; every term of an infinite SRS point is 0) and
-// returns its table entry.  inf may be null: no SRS point is infinite (the
-// table build checks), and no flag is read.
-template <class C, int CB>
-struct FixedTerms {
-  static constexpr int PW = packed_words<C>();
-  static constexpr int W = FixedWin<C, CB>::W;
-  static constexpr uint32_t H = FixedWin<C, CB>::H;
-  const uint32_t* sc;
-  const uint8_t* inf;
-  const uint32_t* tab;
-  TabStrides ts;
-  uint32_t i, T;
-  int w;
-  uint32_t s[8], carry;
-  bool skip;
+// y or 2m - y (a negative digit: -(x, y) = (x, 2m - y), f29_neg_lazy), as
+// per-limb selects: no branch, so no register merge after it
+template <class C>
+KZGX_DEV void affine_cond_neg(Affine<C>& a, uint32_t neg) {
+  using F = typename C::Fp29;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) a.y.v[i] = neg ? F::P2B[i] - a.y.v[i] : a.y.v[i];
+}
 
-  KZGX_DEV void load() {
-    scalar_load(sc + (size_t)i * 8, s);
-    scalar_reduce<C>(s);
-    carry = 0;
-    skip = inf != nullptr && inf[i] != 0;
-    w = 0;
-  }
-  // only while terms remain
-  KZGX_DEV const uint32_t* next(int& d) {
-    if (w == W) {
-      i += T;
-      load();
-    }
-    const int dd = next_digit<CB>(s, carry);
-    d = skip ? 0 : dd;
-    const uint32_t* p = tab + (size_t)i * ts.is + (size_t)w * ts.ws + (size_t)((d < 0 ? -d : d) - (d != 0)) * PW;
-    w++;
-    return p;
-  }
-};
-
-#ifndef KZGX_FIXED_PF
-#define KZGX_FIXED_PF 1
-#endif
-
-// thread t of MSM b sums its terms (FixedTerms) into one XYZZ accumulator
-// with mixed additions (variant V, curve.hpp).  Software pipeline: the
-// table lookups of the next PF terms are in flight during each addition.
-template <class C, int CB, int V = madd_variant<C>(), int PF = KZGX_FIXED_PF>
+// Batched fixed-base accumulation.  Thread t of MSM b sums the W odd-digit
+// terms (odd_digit) of points i = t, t + T, t + 2T, ... into one XYZZ
+// accumulator with mixed additions (variant V, curve.hpp); a wavefront reads
+// 64 consecutive scalars per point step.  Every term is one addition (odd
+// digits are never zero), and the control flow is uniform across the
+// wavefront: the first n / T points of every lane run as one loop whose trip
+// count and window index live in scalar registers (the point change is a
+// uniform branch), and the lanes with one more point run it afterwards.  The
+// loop body is then straight-line code around the addition, so the
+// accumulator and the in-flight table entry stay in their loop registers
+// (the divergent zero-digit branch and per-lane trip counts of round 3 cost
+// ~135 register copies per term).  The table lookup of the next term is in
+// flight during each addition; the next point's scalar is loaded a whole
+// point ahead.
+//
+// inf (null when no SRS point of the prefix is infinite): an infinite point
+// P_i contributes O whatever its scalar, so its terms are replaced by those
+// of scalar 0 on the finite point fin0 -- odd digits of r, which sum to
+// r P_fin0 = O through exact additions.  Selects at the point change, no
+// branch in the loop.
+template <class C, int CB, int V = madd_variant<C>()>
 __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
     const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
-    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t T, uint32_t* __restrict__ part) {
+    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t fin0, uint32_t T, uint32_t* __restrict__ part) {
   constexpr int XW = xyzz_words<C>();
-  using G = FixedTerms<C, CB>;
+  constexpr int PW = packed_words<C>();
+  constexpr int W = FixedWin<C, CB>::W;
   const uint32_t b = blockIdx.y;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
+  if (t >= T) return;  // T is a multiple of 64: whole wavefronts
   Xyzz<C> acc = xyzz_inf<C>();
-  const uint32_t npts = t < n ? (n - 1 - t) / T + 1 : 0;
-  const int E = (int)npts * G::W;
-  if constexpr (PF == 0) {
-    // LDS ring: the next term's entry goes global -> LDS directly
-    // (global_load_lds_dwordx4, per-lane source, lane-linear destination),
-    // so no VGPR holds an in-flight entry; the current one is read back
-    // with ds_read_b128 at the top of each addition
-    constexpr int NCH = G::PW / 4;
-    __shared__ uint4 ring[2][NCH][64];
-    const uint32_t lane = threadIdx.x & 63;
-    if (E > 0) {
-      G g;
-      g.sc = scalars + (size_t)b * stride_words;
-      g.inf = inf;
-      g.tab = tab;
-      g.ts = ts;
-      g.i = t;
-      g.T = T;
-      g.load();
-      auto issue = [&](int slot, const uint32_t* src) {
+  const uint32_t nmin = n / T;                                  // points of every lane
+  const bool extra = t < n - nmin * T;                          // one more point
+  if (nmin > 0 || extra) {
+    const uint32_t* sc = scalars + (size_t)b * stride_words;
+    const uint32_t last = n - 1;
+    uint32_t i = t;
+    uint32_t s[8], sn[8];
+    // point i's table row and its scalar in s: u and the sign flip (an
+    // infinite point becomes scalar 0 on point fin0)
+    const uint32_t* prow;
+    uint32_t flip;
+    auto point = [&](uint32_t ii) __attribute__((always_inline)) {
+      if (inf != nullptr) {  // uniform
+        const bool z = inf[ii] != 0;
 #pragma unroll
-        for (int k = 0; k < NCH; k++)
-          __builtin_amdgcn_global_load_lds((kzgx_gptr_t)(src + 4 * k), (kzgx_lptr_t)&ring[slot][k][0], 16, 0, 0);
-      };
-      int dn = 0;
-      issue(0, g.next(dn));
-#pragma unroll 1
-      for (int e = 0; e < E; e++) {
-        const int slot = e & 1;
-        PackedPt<C> pk;
-#pragma unroll
-        for (int k = 0; k < NCH; k++) pk.q[k] = ring[slot][k][lane];
-        Affine<C> cur = packed_unpack<C>(pk);
-        const int d = dn;
-        if (e + 1 < E) issue(slot ^ 1, g.next(dn));
-        if (d != 0) {
-          if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
-          acc = xyzz_add_affine_v<C, V>(acc, cur);
-        }
+        for (int k = 0; k < 8; k++) s[k] = z ? 0u : s[k];
+        ii = z ? fin0 : ii;
       }
-    }
-  } else {
-   if (E > 0) {
-    G g;
-    g.sc = scalars + (size_t)b * stride_words;
-    g.inf = inf;
-    g.tab = tab;
-    g.ts = ts;
-    g.i = t;
-    g.T = T;
-    g.load();
-    int dq[PF];
-    PackedPt<C> pq[PF];
-#pragma unroll
-    for (int k = 0; k < PF; k++) {
-      dq[k] = 0;
-      if (k < E) pq[k] = packed_fetch<C>(g.next(dq[k]));
-    }
-    // one term: add the queued entry, queue the lookup PF terms ahead
-    auto step = [&](int e) {
-      Affine<C> cur = packed_unpack<C>(pq[0]);
-      const int d = dq[0];
-#pragma unroll
-      for (int k = 0; k + 1 < PF; k++) {
-        pq[k] = pq[k + 1];
-        dq[k] = dq[k + 1];
-      }
-      dq[PF - 1] = 0;
-      if (e + PF < E) pq[PF - 1] = packed_fetch<C>(g.next(dq[PF - 1]));
-      if (d != 0) {
-        // -T = (x, 2m - y): one v_sub per limb (f29_neg_lazy; the
-        // mixed add only multiplies y and feeds it to carry-absorbing subs)
-        if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
-        acc = xyzz_add_affine_v<C, V>(acc, cur);
-      }
+      scalar_reduce<C>(s);
+      flip = odd_prepare<C>(s);
+      prow = tab + (size_t)ii * ts.is;
     };
-    // (a two-term body, for the allocator to alternate the accumulator
-    // between two register sets instead of copying it back, spilled: 368 B
-    // of scratch on BN254, 704 B on BLS12-381)
+    scalar_load(sc + (size_t)(i < last ? i : last) * 8, s);
+    point(i < last ? i : last);
+    {
+      const uint32_t i2 = i + T < last ? i + T : last;
+      scalar_load(sc + (size_t)i2 * 8, sn);
+    }
+    // entry (w, j) of term (i, w) from the low bits of s (s consumed by CB
+    // bits); w is uniform
+    auto fetch = [&](int w, uint32_t& neg) __attribute__((always_inline)) {
+      uint32_t j;
+      odd_digit<CB>(s[0], w == W - 1, flip, j, neg);
+      shr_scalar<CB>(s);
+      return packed_fetch<C>(prow + (size_t)w * ts.ws + (size_t)j * PW);
+    };
+    uint32_t nq;
+    PackedPt<C> pq = fetch(0, nq);
+    int w = 0;
+    // one term: add the queued entry, queue the next term's lookup
+    auto step = [&]() __attribute__((always_inline)) {
+      Affine<C> cur = packed_unpack<C>(pq);
+      const uint32_t neg = nq;
+      if (w == W - 1) {  // uniform: the next term is window 0 of the next point
+        w = 0;
+        i += T;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s[k] = sn[k];
+        point(i < last ? i : last);
+        const uint32_t i2 = i + T < last ? i + T : last;
+        scalar_load(sc + (size_t)i2 * 8, sn);
+      } else {
+        w++;
+      }
+      pq = fetch(w, nq);
+      affine_cond_neg<C>(cur, neg);
+      acc = xyzz_add_affine_v<C, V>(acc, cur);
+    };
+    const uint32_t E = nmin * (uint32_t)W;
 #pragma unroll 1
-    for (int e = 0; e < E; e++) step(e);
-   }
+    for (uint32_t e = 0; e < E; e++) step();
+    if (extra) {
+#pragma unroll 1
+      for (int e = 0; e < W; e++) step();
+    }
   }
   xyzz_store<C>(part + ((size_t)b * T + t) * XW, acc);
 }

@@ -74,8 +74,9 @@ class WsLease {
 
 constexpr int KZGX_MAX_STREAMS = 8;
 
-// precomputed signed-digit multiples of the SRS prefix (msm_fixed.hip):
-// M[w][i][j] = (j + 1) 2^(c w) P_i, packed affine, w < W, i < n_t, j < 2^(c-1)
+// precomputed odd multiples of the SRS prefix (msm_fixed.hip, indexed by
+// the regular odd digits of fixed_accum.hpp):
+// M[w][i][j] = (2 j + 1) 2^(c w) P_i, packed affine, w < W, i < n_t, j < 2^(c-1)
 struct FixedTable {
   int c_req = 0;        // requested window bits (0 = off)
   size_t n_req = 0;     // requested SRS prefix length
@@ -88,6 +89,7 @@ struct FixedTable {
   size_t bytes = 0;
   uint8_t* inf = nullptr;  // [n_t] infinite SRS points (skipped)
   bool any_inf = true;     // some flag of inf is set (else the kernels get no flags)
+  uint32_t fin0 = UINT32_MAX;  // first finite point of the prefix (k_fixed_accum's identity terms)
 };
 
 // optional per-kernel timing with HIP events on the launch stream

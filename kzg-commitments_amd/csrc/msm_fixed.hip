@@ -35,9 +35,9 @@
 
 namespace kzgx {
 
-int fixed_windows(int curve, int c) {
+int fixed_windows(int curve, int c) {  // FixedWin<C, c>::W (regular odd digits)
   const int bits = curve == KZGX_CURVE_BN254 ? BN254G1::SCALAR_BITS : BLS12381G1::SCALAR_BITS;
-  return (bits + 1 + c - 1) / c;
+  return (bits + c - 1) / c;
 }
 
 // --------------------------------------------------------------------------
@@ -63,7 +63,8 @@ __global__ __launch_bounds__(64) void k_fixed_bases(const uint32_t* __restrict__
   }
 }
 
-// M(w, i, j0 + j) = (j0 + j + 1) B[w][i], j < J; thread per (w, i, block),
+// M(w, i, j0 + j) = (2 (j0 + j) + 1) B[w][i], j < J (the odd multiples the
+// regular odd digits index, fixed_accum.hpp); thread per (w, i, block),
 // written at the table's strides (TabStrides)
 template <class C>
 __global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restrict__ bases,
@@ -85,17 +86,19 @@ __global__ __launch_bounds__(64) void k_fixed_multiples(const uint32_t* __restri
     return;
   }
   const Affine<C> B = packed_load<C>(bases + wi * PW);
-  const uint32_t k0 = blk * J + 1;
+  Affine<C> B2;  // 2 B (!= O: B has order r > 2)
+  xyzz_to_affine<C>(xyzz_dbl<C>(xyzz_from_affine<C>(B)), B2);
+  const uint32_t k0 = 2 * blk * J + 1;
   // acc = k0 B, left-to-right double-and-add
   Xyzz<C> acc = xyzz_from_affine<C>(B);
-  for (int bit = 30 - __builtin_clz(k0) ; bit >= 0; bit--) {
+  for (int bit = 30 - __builtin_clz(k0); bit >= 0; bit--) {
     acc = xyzz_dbl<C>(acc);
     if ((k0 >> bit) & 1u) acc = xyzz_add_affine<C>(acc, B);
   }
   for (uint32_t j = 0; j < J; j++) {
-    if (j) acc = xyzz_add_affine<C>(acc, B);
+    if (j) acc = xyzz_add_affine<C>(acc, B2);
     Affine<C> a;
-    xyzz_to_affine<C>(acc, a);  // (k0 + j) B != O since k0 + j <= H < r
+    xyzz_to_affine<C>(acc, a);  // (k0 + 2 j) B != O since k0 + 2 j < 2 H <= 2^17 < r
     packed_store<C>(out + (size_t)j * PW, a);
   }
 }
@@ -196,15 +199,17 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
       s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
     }
     scalar_reduce<C>(s);
+    const uint32_t flip = odd_prepare<C>(s);
     const uint32_t* base = tab + (size_t)i * ts.is;
-    uint32_t carry = 0;
 #pragma unroll 1
-    for (int w = 0; w < w1; w++) {
-      const int d = next_digit<CB>(s, carry);  // windows below w0 only carry
-      if (w < w0 || d == 0) continue;
-      Affine<C> cur =
-          packed_unpack<C>(packed_fetch<C>(base + (size_t)w * ts.ws + (size_t)((d < 0 ? -d : d) - 1) * PW));
-      if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
+    for (int w = 0; w < w0; w++) shr_scalar<CB>(s);  // odd digits carry nothing: skip the lower windows
+#pragma unroll 1
+    for (int w = w0; w < w1; w++) {
+      uint32_t j, neg;
+      odd_digit<CB>(s[0], w == W - 1, flip, j, neg);
+      shr_scalar<CB>(s);
+      Affine<C> cur = packed_unpack<C>(packed_fetch<C>(base + (size_t)w * ts.ws + (size_t)j * PW));
+      affine_cond_neg<C>(cur, neg);
       acc = xyzz_add_affine_impl<C>(acc, cur);
     }
   }
@@ -265,57 +270,63 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
   const size_t e1 = e + Q < e_end ? e + Q : e_end;
   Xyzz<C> acc = xyzz_inf<C>();
   if (e < e1) {
-    // generator state: point i, window w, the scalar's remaining bits
+    // generator state: point i, window w, the remaining bits of u (odd
+    // digits, fixed_accum.hpp) and the sign flip of the point's scalar
     uint32_t i = (uint32_t)(e / W);
     int w = (int)(e - (size_t)i * W);
-    uint32_t s[8], carry = 0;
+    uint32_t s[8], flip = 0;
     bool skip = false;  // infinity SRS point: all its terms are the identity
     auto load = [&](uint32_t ii) {
       scalar_load(sc + (size_t)ii * 8, s);
       scalar_reduce<C>(s);
-      carry = 0;
+      flip = odd_prepare<C>(s);
       skip = inf != nullptr && inf[ii] != 0;
     };
     load(i);
 #pragma unroll 1
-    for (int k = 0; k < w; k++) (void)next_digit<CB>(s, carry);  // carry of the lower windows
-    // the digit of the current term and its table entry's address
-    auto fetch = [&](int dd) {
-      return packed_fetch<C>(tab + (size_t)i * ts.is + (size_t)w * ts.ws +
-                             (size_t)((dd < 0 ? -dd : dd) - (dd != 0)) * PW);
+    for (int k = 0; k < w; k++) shr_scalar<CB>(s);  // no carry: the lower windows are skipped outright
+    // the table entry of the current term (i, w); consumes its window bits
+    struct Term {
+      PackedPt<C> p;
+      uint32_t neg;
+      bool skip;
+    };
+    auto fetch = [&]() {
+      Term r;
+      uint32_t j;
+      odd_digit<CB>(s[0], w == W - 1, flip, j, r.neg);
+      shr_scalar<CB>(s);
+      r.skip = skip;
+      r.p = packed_fetch<C>(tab + (size_t)i * ts.is + (size_t)w * ts.ws + (size_t)j * PW);
+      return r;
     };
     auto advance = [&]() {
       if (++w == W) {
         w = 0;
         load(++i);
       }
-      const int dd = next_digit<CB>(s, carry);
-      return skip ? 0 : dd;
     };
-    int d0 = next_digit<CB>(s, carry);
-    if (skip) d0 = 0;
-    PackedPt<C> p0 = fetch(d0);
+    Term t0 = fetch();
     // two lookups in flight: terms e + 1 and e + 2 load during the addition
     // of term e (one wave in three is ready to issue while the other two wait
     // on random table lines)
-    int d1 = 0;
-    PackedPt<C> p1 = p0;
+    Term t1 = t0;
     if (e + 1 < e1) {
-      d1 = advance();
-      p1 = fetch(d1);
+      advance();
+      t1 = fetch();
     }
 #pragma unroll 1
     for (; e < e1; e++) {
-      Affine<C> cur = packed_unpack<C>(p0);
-      const int d = d0;
-      d0 = d1;
-      p0 = p1;
+      Affine<C> cur = packed_unpack<C>(t0.p);
+      const uint32_t neg = t0.neg;
+      const bool sk = t0.skip;
+      t0 = t1;
       if (e + 2 < e1) {
-        d1 = advance();
-        p1 = fetch(d1);
+        advance();
+        t1 = fetch();
       }
-      if (d != 0) {
-        if (d < 0) cur.y = f29_neg_lazy<typename C::Fp29>(cur.y);
+      if (!sk) {
+        affine_cond_neg<C>(cur, neg);
         acc = xyzz_add_affine_impl<C>(acc, cur);
       }
     }
@@ -424,6 +435,8 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
     KZGX_TRY_HIP(hipMemcpyAsync(h.data(), d_inf, n, hipMemcpyDeviceToHost, st));
     KZGX_TRY_HIP(hipStreamSynchronize(st));
     ft.any_inf = std::any_of(h.begin(), h.end(), [](uint8_t v) { return v != 0; });
+    const auto f = std::find(h.begin(), h.end(), (uint8_t)0);
+    ft.fin0 = f == h.end() ? UINT32_MAX : (uint32_t)(f - h.begin());
   }
   g.ok = true;
   ft.inf = d_inf;
@@ -450,6 +463,7 @@ void fixed_free(Ctx* ctx) {
   ft.bytes = 0;
   ft.n_t = 0;
   ft.c = 0;
+  ft.fin0 = UINT32_MAX;
 }
 
 template <class C, int CB>
@@ -542,7 +556,7 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
   {
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                       (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), T, ws.fpart);
+                       (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), ft.fin0, T, ws.fpart);
   }
   if (wave_red) {
     ProfScope p(ctx, st, "msm_reduce");
@@ -613,7 +627,11 @@ bool fixed_bits_supported(int c) {
   return c == 0 || c == 4 || (c >= 7 && c <= 17);
 }
 
-bool fixed_usable(const Ctx* ctx, size_t n) { return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t; }
+// (a prefix of infinite points only -- a loaded all-infinity SRS -- has no
+// finite point to carry the identity terms of k_fixed_accum: Pippenger)
+bool fixed_usable(const Ctx* ctx, size_t n) {
+  return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t && ctx->fixed.fin0 != UINT32_MAX;
+}
 
 int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {

@@ -128,14 +128,14 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
     for (int rep = 0; rep < 3; rep++) {
       hipEventRecord(e0, 0);
       if (v == 0)
-        hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, nullptr, T, d_p0);
+        hipLaunchKernelGGL((k_fixed_accum<C, CB, 0>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
+                           ts, nullptr, 0u, T, d_p0);
       else if (v == 1)
-        hipLaunchKernelGGL((k_fixed_accum<C, CB, 1, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, nullptr, T, d_p1);
+        hipLaunchKernelGGL((k_fixed_accum<C, CB, 1>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
+                           ts, nullptr, 0u, T, d_p1);
       else  // loads and digit recoding only: the memory path's own rate
-        hipLaunchKernelGGL((k_fixed_accum<C, CB, 2, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
-                           ts, nullptr, T, d_p0 + 0 * pw);
+        hipLaunchKernelGGL((k_fixed_accum<C, CB, 2>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab,
+                           ts, nullptr, 0u, T, d_p0 + 0 * pw);
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float m = 0;
@@ -144,8 +144,8 @@ static int run_accum(const char* name, uint32_t B, uint32_t ppt) {
     }
   }
   // rerun classic into d_p0 (the probe overwrote it)
-  hipLaunchKernelGGL((k_fixed_accum<C, CB, 0, PF>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab, ts,
-                     d_inf, T, d_p0);
+  hipLaunchKernelGGL((k_fixed_accum<C, CB, 0>), dim3(T / 64, B), dim3(64), 0, 0, d_sc, n, (size_t)n * 8, d_tab, ts,
+                     d_inf, 0u, T, d_p0);
   std::vector<uint32_t> h0(pw), h1(pw);
   hipMemcpy(h0.data(), d_p0, pw * 4, hipMemcpyDeviceToHost);
   hipMemcpy(h1.data(), d_p1, pw * 4, hipMemcpyDeviceToHost);

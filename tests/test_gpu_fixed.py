@@ -324,3 +324,35 @@ def test_clock_measurements_read_a_plausible_core_clock():
             ctx.clock_probe(buf.data_ptr(), 0)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("c", [7, 16, 17])
+def test_odd_digit_edges(name, C, c, fresh_ctx):
+    """Regular odd digits (fixed_accum.hpp): even scalars run as r - k with
+    every digit negated, 0 becomes r (terms summing to O), and the extreme
+    windows -- u's window bits all zero (digit 1 - 2^c) or all one (digit
+    2^c - 1), the top digit at its largest -- index the first and last
+    odd multiple.  Batched kernel (batch 20) and latency kernel (batch 1)."""
+    ctx = fresh_ctx(name)
+    tau = K.default_tau(C)
+    n = 40
+    ctx.gen_srs(tau, n)
+    ctx.set_fixed_base(c, n)
+    W = (C.r.bit_length() + c - 1) // c
+    ones = sum(((1 << c) - 1) << (c * w) for w in range(W - 1))  # u windows all ones
+    edge = [0, 1, 2, 3, C.r - 1, C.r - 2, C.r - 3, 2 * ones + 1, (2 * ones + 1) % C.r,
+            (1 << (C.r.bit_length() - 1)) + 1, C.r - (2 * ones + 1) % C.r, 5, 1 << 200]
+    polys = []
+    for b in range(20):
+        P = K.random_scalars(C, n, seed=5100 + b)
+        for j, v in enumerate(edge):
+            P[(j + b) % n] = v % C.r
+        polys.append(P)
+    S = np.concatenate([limbs(P) for P in polys])
+    out, inf = ctx.msm_batch(S, n, len(polys))
+    for b in range(len(polys)):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+    ctx.set_fixed_points_per_thread(0)
+    out1, inf1 = ctx.msm(limbs(polys[3]))
+    assert pt(name, out1, inf1) == K.commit_via_tau(C, tau, polys[3])
