@@ -27,6 +27,16 @@
 // time) without helping the scheduler.  The hot loop uses the _impl forms.
 #define KZGX_PT __device__ __noinline__
 
+// Assembly comments that scripts/isa_count.py uses to find the rare paths
+// (first term after infinity, equal x) and the per-point work of the
+// accumulation loops.  Only with -DKZGX_ISA_MARKERS (the counting build): an
+// asm statement is a scheduling barrier, so production code has none.
+#ifdef KZGX_ISA_MARKERS
+#define KZGX_MARK(s) asm volatile(";" s)
+#else
+#define KZGX_MARK(s)
+#endif
+
 // -Y1 in the mixed add's Y3: carry-free 8m - Y1 (f29_neg8_lazy) or the
 // carried 4m - Y1.  The lazy form saves ~25 VALU instructions but makes the
 // compiler spill around the rare P == +-a branch of the fixed-base kernel.
@@ -162,7 +172,10 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_classic(const Xyzz<C>& p, const Affine<C>& a) {
     return r;
   }
 #else
-  if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
+  if (xyzz_is_inf<C>(p)) {
+    KZGX_MARK("KZGX_RARE");
+    return xyzz_from_affine<C>(a);
+  }
 #endif
   F29<F> U2 = f29_mul<F>(a.x, p.ZZ);                    // < 2m
   F29<F> S2 = f29_mul<F>(a.y, p.ZZZ);                   // < 2m
@@ -170,6 +183,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_classic(const Xyzz<C>& p, const Affine<C>& a) {
   F29<F> R = f29_sub<F>(S2, p.Y, F::P4);                // < 6m
   F29<F> PP = f29_sqr<F>(P);                            // < 2m
   if (f29_is_zero_lt2m<F>(PP)) {                        // x equal: double or cancel
+    KZGX_MARK("KZGX_RARE");
     if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);  // inline: no call frame in the hot loop
     return xyzz_inf<C>();
   }
@@ -207,7 +221,10 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
     return r;
   }
 #else
-  if (xyzz_is_inf<C>(p)) return xyzz_from_affine<C>(a);
+  if (xyzz_is_inf<C>(p)) {
+    KZGX_MARK("KZGX_RARE");
+    return xyzz_from_affine<C>(a);
+  }
 #endif
   F29<F> U2, S2;
 #ifdef KZGX_NWAY_TRI
@@ -219,6 +236,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
   F29<F> PP, RR;
   f29_sqr_x2<F>(P, R, PP, RR);                   // < 2m each
   if (f29_is_zero_lt2m<F>(PP)) {
+    KZGX_MARK("KZGX_RARE");
     if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);
     return xyzz_inf<C>();
   }
@@ -239,6 +257,7 @@ KZGX_DEV Xyzz<C> xyzz_add_affine_nway(const Xyzz<C>& p, const Affine<C>& a) {
   const F29<F> R = f29_sub<F>(S2, p.Y, F::P4);          // < 6m
   const F29<F> PP = f29_sqr_chain<F>(P);                // < 2m
   if (f29_is_zero_lt2m<F>(PP)) {  // x equal: double or cancel
+    KZGX_MARK("KZGX_RARE");
     if (f29_is_zero<F>(R)) return xyzz_dbl_affine_impl<C>(a);
     return xyzz_inf<C>();
   }

@@ -314,6 +314,7 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum(
       Affine<C> cur = packed_unpack<C>(pq);
       const uint32_t neg = nq;
       if (w == W - 1) {  // uniform: the next term is window 0 of the next point
+        KZGX_MARK("KZGX_PER_POINT");
         w = 0;
         i += T;
 #pragma unroll

@@ -34,6 +34,14 @@ struct kzgx_ctx {
   uint32_t* d_g2tab = nullptr;
   size_t g2tab_b = 0;
   size_t g2tab_n = 0;  // points covered; 0 = stale
+  // pinned, device-mapped host staging for the host-pointer entry points
+  // (kzgx_msm_g1_batch, kzgx_prove_single_batch): inputs are copied into it
+  // and read by the kernels in place (small) or DMA'd from it (large); the
+  // last kernel of a call writes its results straight into it, so a call
+  // makes no device-to-host copy and synchronises once
+  uint8_t* h_pin = nullptr;
+  uint8_t* d_pin = nullptr;  // device address of h_pin
+  size_t pin_b = 0;
 };
 
 namespace kzgx {
@@ -87,6 +95,36 @@ int stage(kzgx_ctx* ctx, int slot, size_t bytes, void** out) {
 }
 
 size_t point_words(const kzgx_ctx* ctx) { return 2 * (size_t)ctx->c.base_words(); }
+
+// the context's pinned mapped staging of at least `bytes` (grow-only)
+int pin_stage(kzgx_ctx* ctx, size_t bytes) {
+  if (ctx->h_pin && bytes <= ctx->pin_b) return KZGX_OK;
+  if (ctx->h_pin) {
+    KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+    (void)hipHostFree(ctx->h_pin);
+    ctx->h_pin = ctx->d_pin = nullptr;
+    ctx->pin_b = 0;
+  }
+  const size_t want = std::max<size_t>(bytes + bytes / 8, (size_t)1 << 20);
+  void* h = nullptr;
+  KZGX_TRY_HIP(hipHostMalloc(&h, want, hipHostMallocMapped | hipHostMallocCoherent));
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return kzgx::hip_fail(e);
+  }
+  ctx->h_pin = static_cast<uint8_t*>(h);
+  ctx->d_pin = static_cast<uint8_t*>(d);
+  ctx->pin_b = want;
+  return KZGX_OK;
+}
+
+// kernels read inputs up to this size straight from the mapped staging
+// (PCIe reads, no copy launch); larger inputs are DMA'd to device memory
+constexpr size_t PIN_DIRECT_MAX = (size_t)256 << 10;
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // x mod r for a 4 x 64-bit little-endian value: the reference converts its
 // evaluation points into ZZ_p (src/trusted_setup.cpp:214-219), so x and x + r
@@ -174,11 +212,13 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   kzgx::fixed_free(&c);
   for (auto& w : c.ws) {
     void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
-                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig};
+                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig,
+                  w.ebm};
     for (void* p : wb)
       if (p) (void)hipFree(p);
     if (w.done) (void)hipEventDestroy(w.done);
   }
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   (void)hipStreamDestroy(c.stream);
   delete ctx;
 }
@@ -431,17 +471,25 @@ int kzgx_msm_g1_batch(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, size_t b
   if (!out_xy || !out_is_inf || (n > 0 && !scalars)) return KZGX_ERR_ARG;
   if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
   if (n > ctx->c.n_srs) return KZGX_ERR_DEGREE;
-  void *d_s = nullptr, *d_o, *d_i;
   const size_t sb = n * batch * 32, ob = batch * point_words(ctx) * 4;
-  if (n) KZGX_TRY(stage(ctx, 0, sb, &d_s));
-  KZGX_TRY(stage(ctx, 1, ob, &d_o));
-  KZGX_TRY(stage(ctx, 2, batch * 4, &d_i));
-  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, ctx->c.stream));
-  KZGX_TRY(kzgx_msm_g1_batch_device(ctx, d_s, n, batch, n, d_o, d_i, nullptr));
-  std::vector<uint32_t> inf(batch);
-  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, ob, hipMemcpyDeviceToHost, ctx->c.stream));
-  KZGX_TRY_HIP(hipMemcpyAsync(inf.data(), d_i, batch * 4, hipMemcpyDeviceToHost, ctx->c.stream));
+  // pinned layout: [results | flags | scalars]; results are written by the
+  // last kernel into mapped host memory (no D2H copy)
+  const size_t o_off = 0, i_off = align256(ob), s_off = i_off + align256(batch * 4);
+  KZGX_TRY(pin_stage(ctx, s_off + sb));
+  void* d_s = nullptr;
+  if (n) {
+    std::memcpy(ctx->h_pin + s_off, scalars, sb);
+    if (sb <= PIN_DIRECT_MAX) {
+      d_s = ctx->d_pin + s_off;
+    } else {
+      KZGX_TRY(stage(ctx, 0, sb, &d_s));
+      KZGX_TRY_HIP(hipMemcpyAsync(d_s, ctx->h_pin + s_off, sb, hipMemcpyHostToDevice, ctx->c.stream));
+    }
+  }
+  KZGX_TRY(kzgx_msm_g1_batch_device(ctx, d_s, n, batch, n, ctx->d_pin + o_off, ctx->d_pin + i_off, nullptr));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  std::memcpy(out_xy, ctx->h_pin + o_off, ob);
+  const uint32_t* inf = reinterpret_cast<const uint32_t*>(ctx->h_pin + i_off);
   for (size_t b = 0; b < batch; b++) out_is_inf[b] = (int)inf[b];
   return KZGX_OK;
 }
@@ -562,21 +610,29 @@ int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, siz
   const size_t npolys = coeff_stride == 0 ? 1 : batch;
   const size_t cb = (npolys - 1) * coeff_stride * 32 + n * 32;
   const size_t ob = batch * point_words(ctx) * 4;
-  void *d_c = nullptr, *d_z, *d_o, *d_i, *d_y;
-  if (n) KZGX_TRY(stage(ctx, 0, cb, &d_c));
-  KZGX_TRY(stage(ctx, 1, ob + batch * 4, &d_o));
-  d_i = (char*)d_o + ob;
-  KZGX_TRY(stage(ctx, 2, batch * 64, &d_z));
-  d_y = (char*)d_z + batch * 32;
-  if (n) KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, cb, hipMemcpyHostToDevice, ctx->c.stream));
-  KZGX_TRY_HIP(hipMemcpyAsync(d_z, zs, batch * 32, hipMemcpyHostToDevice, ctx->c.stream));
-  KZGX_TRY(kzgx_prove_single_batch_device(ctx, d_c, n, coeff_stride, d_z, batch, d_o, d_i, d_y, nullptr));
-  std::vector<uint32_t> inf(batch);
-  KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_o, ob, hipMemcpyDeviceToHost, ctx->c.stream));
-  KZGX_TRY_HIP(hipMemcpyAsync(inf.data(), d_i, batch * 4, hipMemcpyDeviceToHost, ctx->c.stream));
-  if (out_y) KZGX_TRY_HIP(hipMemcpyAsync(out_y, d_y, batch * 32, hipMemcpyDeviceToHost, ctx->c.stream));
+  // pinned layout: [results | flags | y | z | coefficients]; outputs are
+  // written by the kernels into mapped host memory (no D2H copies)
+  const size_t o_off = 0, i_off = align256(ob), y_off = i_off + align256(batch * 4),
+               z_off = y_off + align256(batch * 32), c_off = z_off + align256(batch * 32);
+  KZGX_TRY(pin_stage(ctx, c_off + cb));
+  std::memcpy(ctx->h_pin + z_off, zs, batch * 32);
+  void* d_c = nullptr;
+  if (n) {
+    std::memcpy(ctx->h_pin + c_off, coeffs, cb);
+    if (cb <= PIN_DIRECT_MAX) {
+      d_c = ctx->d_pin + c_off;
+    } else {
+      KZGX_TRY(stage(ctx, 0, cb, &d_c));
+      KZGX_TRY_HIP(hipMemcpyAsync(d_c, ctx->h_pin + c_off, cb, hipMemcpyHostToDevice, ctx->c.stream));
+    }
+  }
+  KZGX_TRY(kzgx_prove_single_batch_device(ctx, d_c, n, coeff_stride, ctx->d_pin + z_off, batch, ctx->d_pin + o_off,
+                                          ctx->d_pin + i_off, ctx->d_pin + y_off, nullptr));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  std::memcpy(out_xy, ctx->h_pin + o_off, ob);
+  const uint32_t* inf = reinterpret_cast<const uint32_t*>(ctx->h_pin + i_off);
   for (size_t b = 0; b < batch; b++) out_is_inf[b] = (int)inf[b];
+  if (out_y) std::memcpy(out_y, ctx->h_pin + y_off, batch * 32);
   return KZGX_OK;
 }
 

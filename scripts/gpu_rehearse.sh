@@ -15,3 +15,8 @@ tail -c 300 "$OUT/cfg2_2rank.json"
 timeout -k 10 500 python -u bench.py --gpus 2 --workload cfg5 --steps 5 --warmup 1 --table-gb 60 --no-cpu-baseline \
   > "$OUT/cfg5_2rank.json" 2> "$OUT/cfg5_2rank.err" || { tail -20 "$OUT/cfg5_2rank.err"; exit 1; }
 tail -c 300 "$OUT/cfg5_2rank.json"
+# strong scaling: a fixed total batch split over the ranks
+timeout -k 10 500 python -u bench.py --gpus 2 --scaling strong --global-batch 4096 --steps 5 --warmup 1 --fixed-bits 12 \
+  --no-cpu-baseline --no-pippenger --no-latency --no-table-curve > "$OUT/cfg2_2rank_strong.json" \
+  2> "$OUT/cfg2_2rank_strong.err" || { tail -20 "$OUT/cfg2_2rank_strong.err"; exit 1; }
+tail -c 300 "$OUT/cfg2_2rank_strong.json"

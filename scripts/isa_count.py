@@ -73,7 +73,9 @@ def hot_loop(body):
         if m and m.group(2) in labels and labels[m.group(2)] < i:
             lo = labels[m.group(2)]
             mads = sum(1 for x in body[lo:i] if "v_mad_u64_u32" in x)
-            if best is None or mads > best[0]:
+            # most mads; among equal counts the tightest loop (an outer loop
+            # around the term loop holds the same mads)
+            if best is None or mads > best[0] or (mads == best[0] and i - lo < best[2] - best[1]):
                 best = (mads, lo, i)
     if best is None:
         raise SystemExit("no loop found")
@@ -133,6 +135,69 @@ def fallthrough_path(body, lo, hi):
     return out
 
 
+def marked_path(body, lo, hi, per_point):
+    """(line, weight) pairs of one term's steady-state path through the loop
+    [lo, hi], in a build with -DKZGX_ISA_MARKERS (curve.hpp KZGX_MARK): a
+    forward branch whose first guarded block holds ';KZGX_RARE' is taken
+    (the rare body is skipped), one whose first block holds
+    ';KZGX_PER_POINT' guards the point change, counted with weight
+    1 / per_point; every other forward branch falls through (its body runs
+    on the common path).  Unconditional forward jumps are followed."""
+    labels = {}
+    for i in range(lo, hi + 1):
+        m = LABEL.match(body[i])
+        if m:
+            labels[m.group(1)] = i
+
+    def first_block(i):
+        """the guarded region's lines outside every region nested in it (an
+        asm marker may be scheduled anywhere in its block, not only first)"""
+        tgt = labels[BRANCH.match(body[i]).group(2)]
+        out = []
+        j = i + 1
+        while j < tgt:
+            m = BRANCH.match(body[j])
+            if m and m.group(2) in labels and j < labels[m.group(2)] <= tgt:
+                j = labels[m.group(2)]  # skip the nested region
+                continue
+            out.append(body[j])
+            j += 1
+        return out
+
+    out = []
+    i = lo
+    while i <= hi:
+        ln = body[i]
+        m = BRANCH.match(ln)
+        if m and m.group(2) in labels and labels[m.group(2)] > i:
+            tgt = labels[m.group(2)]
+            head = first_block(i)
+            if m.group(1) == "s_branch":
+                i = tgt
+                continue
+            if any("KZGX_RARE" in x for x in head):
+                out.append((ln, 1.0))
+                i = tgt
+                continue
+            if any("KZGX_PER_POINT" in x for x in head):
+                out.append((ln, 1.0))
+                out.extend((x, 1.0 / per_point) for x in body[i + 1:tgt])
+                i = tgt
+                continue
+        out.append((ln, 1.0))
+        i += 1
+    return out
+
+
+def weighted_histogram(pairs):
+    h = collections.Counter()
+    for ln, wgt in pairs:
+        m = mnemonic(ln)
+        if m:
+            h[m] += wgt
+    return h
+
+
 VALU_PREFIX = "v_"
 
 
@@ -147,38 +212,59 @@ def summarize(h, per):
     return res
 
 
-KERNELS = {  # bench.py's secondary.mad_issue key -> k_fixed_accum instantiation
-    "BN254_c16": "k_fixed_accumINS_7BN254G1ELi16E",
-    "BN254_c17": "k_fixed_accumINS_7BN254G1ELi17E",
-    "BLS12381_c16": "k_fixed_accumINS_10BLS12381G1ELi16E",
-    "BLS12381_c17": "k_fixed_accumINS_10BLS12381G1ELi17E",
+KERNELS = {  # bench.py's secondary.mad_issue key -> (kernel instantiation, windows per point)
+    "BN254_c16": ("k_fixed_accumINS_7BN254G1ELi16E", 16),
+    "BN254_c17": ("k_fixed_accumINS_7BN254G1ELi17E", 15),
+    "BLS12381_c16": ("k_fixed_accumINS_10BLS12381G1ELi16E", 16),
 }
+
+PROBE = """#include "fixed_accum.hpp"
+namespace kzgx {
+template __global__ void k_fixed_accum<BN254G1, 16>(const uint32_t*, uint32_t, size_t, const uint32_t*, TabStrides,
+                                                    const uint8_t*, uint32_t, uint32_t, uint32_t*);
+template __global__ void k_fixed_accum<BN254G1, 17>(const uint32_t*, uint32_t, size_t, const uint32_t*, TabStrides,
+                                                    const uint8_t*, uint32_t, uint32_t, uint32_t*);
+template __global__ void k_fixed_accum<BLS12381G1, 16>(const uint32_t*, uint32_t, size_t, const uint32_t*,
+                                                       TabStrides, const uint8_t*, uint32_t, uint32_t, uint32_t*);
+}
+"""
 
 
 def emit_profile(out_path):
-    """compile csrc/msm_fixed.hip to gfx950 assembly and write the per-term
-    common-path counts of the table kernels (one mixed addition per term)"""
+    """compile the k_fixed_accum instantiations of the throughput lines with
+    the rare-path markers (-DKZGX_ISA_MARKERS) to gfx950 assembly and write
+    the steady-state instructions per term: the common path of one mixed
+    addition and its fetch / unpack / digit work, plus the point change
+    divided by the windows per point"""
     import os
     import subprocess
     import tempfile
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-    src = os.path.join(root, "kzg-commitments_amd", "csrc", "msm_fixed.hip")
+    csrc = os.path.join(root, "kzg-commitments_amd", "csrc")
     with tempfile.TemporaryDirectory() as tmp:
-        asm = os.path.join(tmp, "msm_fixed.s")
+        src = os.path.join(tmp, "probe.hip")
+        with open(src, "w") as f:
+            f.write(PROBE)
+        asm = os.path.join(tmp, "probe.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
-                        "-S", "-o", asm, src], check=True, capture_output=True)
+                        "-DKZGX_ISA_MARKERS", "-I", csrc, "-S", "-o", asm, src], check=True, capture_output=True)
         with open(asm) as f:
             lines = f.read().splitlines()
     res = {"generated_by": "python3 scripts/isa_count.py --profile " + os.path.relpath(out_path, root),
-           "unit": "instructions per table term (one XYZZ mixed addition plus the term's fetch/unpack/digit "
-                   "work) on the loop's common path: from the loop head to the first conditional back edge "
-                   "after the products (the rare full equality check and doubling are skipped there)"}
-    for key, needle in KERNELS.items():
+           "unit": "instructions per table term in steady state: the loop's path with the rare bodies "
+                   "(accumulator at infinity, equal x) skipped and the point change (scalar load, odd "
+                   "recoding prep, table row) divided by the W windows per point; built with "
+                   "-DKZGX_ISA_MARKERS (asm comments at those branches, curve.hpp KZGX_MARK)"}
+    for key, (needle, W) in KERNELS.items():
         body = kernel_body(lines, needle)
         lo, hi = hot_loop(body)
-        c = summarize(histogram(common_path(body, lo, hi)), 1.0)
-        res[key] = {"v_mad_u64_u32": c["v_mad_u64_u32"], "valu": c["valu"], "salu": c["salu"],
-                    "s_nop": c["top"].get("s_nop", 0), "non_mad_valu": c["valu"] - c["v_mad_u64_u32"]}
+        h = weighted_histogram(marked_path(body, lo, hi, W))
+        valu = sum(v for k, v in h.items() if k.startswith(VALU_PREFIX))
+        mads = h.get("v_mad_u64_u32", 0)
+        res[key] = {"v_mad_u64_u32": round(mads, 2), "valu": round(valu, 2),
+                    "salu": round(sum(v for k, v in h.items() if k.startswith("s_")), 2),
+                    "s_nop": round(h.get("s_nop", 0), 2), "non_mad_valu": round(valu - mads, 2),
+                    "v_mov": round(sum(v for k, v in h.items() if k.startswith("v_mov")), 2)}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

@@ -58,8 +58,9 @@ def digit_edge_scalars(C, c, n, seed):
 @pytest.mark.parametrize("name,C", CURVES)
 @pytest.mark.parametrize("c", [16, 17])
 def test_headline_window_bits(name, C, c):
-    """k_fixed_accum<C, 16> (the bench default) and <C, 17> (its fallback
-    neighbour) on both curves, against the naive per-term MSM."""
+    """k_fixed_accum<C, 17> (the BN254 bench default, cfg2 / cfg3) and
+    <C, 16> (the BLS12-381 default, cfg4, and BN254's fallback when c = 17
+    does not fit) on both curves, against the naive per-term MSM."""
     import corc
     import kzgx
     ctx = kzgx.Context(name)
