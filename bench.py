@@ -795,9 +795,13 @@ def main():
         mpa = mads_per_mixed_add(L)
         isa = None
         try:
-            with open(os.path.join(ROOT, "profiles", "r03_isa_counts.json")) as f:
+            import glob
+            latest = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_isa_counts.json")))[-1]
+            with open(latest) as f:
                 isa = json.load(f).get("%s_c%d" % (curve, fb[0]))
-        except (OSError, ValueError):
+            if isa is not None:
+                isa = dict(isa, source=os.path.relpath(latest, ROOT))
+        except (OSError, ValueError, IndexError):
             isa = None
         line = {
             "metric": "KZG commits/sec + proofs/sec, %s degree-4096" % curve,

@@ -281,18 +281,30 @@ KZGX_DEV void mc_reduce(MontChain<F>& c, F29<F>& r, const uint32_t (&pl)[F::L]) 
   if constexpr (K == 2 * L - 2) r.v[L - 1] = (uint32_t)c.acc;
 }
 
-// the modulus limbs as the opaque uniform values of f29_pl, once per call
+// the modulus limbs of the chained products, once per call: BN254 as the
+// opaque uniform (SGPR) values of f29_pl -- the mads read them as their
+// SGPR operand, where opaque VGPR copies were rematerialised with 14 v_mov
+// per table term (steady-state non-mad VALU 761.9 -> 743.9,
+// scripts/isa_count.py; cfg2 +0.9% interleaved, profiles/r04_ab_pl_sgpr_cfg2.json);
+// BLS12-381 keeps opaque VGPR copies (f29_pl leaves its 14 limbs literal to
+// avoid SGPR spills).  KZGX_PL_VGPR / KZGX_PL_SGPR force one form (A/B).
 template <class F>
 struct PLimbs {
   uint32_t v[F::L];
   KZGX_DEV PLimbs() {
+#if defined(KZGX_PL_SGPR)
+    constexpr bool sg = true;
+#elif defined(KZGX_PL_VGPR)
+    constexpr bool sg = false;
+#else
+    constexpr bool sg = F::L <= 9;
+#endif
 #pragma unroll
     for (int j = 0; j < F::L; j++) {
-#ifdef KZGX_PL_SGPR
-      v[j] = f29_pl<F>(j);
-#else
-      asm("" : "=v"(v[j]) : "0"(F::P[j]));
-#endif
+      if constexpr (sg)
+        v[j] = f29_pl<F>(j);
+      else
+        asm("" : "=v"(v[j]) : "0"(F::P[j]));
     }
   }
 };

@@ -212,8 +212,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   kzgx::fixed_free(&c);
   for (auto& w : c.ws) {
     void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
-                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig,
-                  w.ebm};
+                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig};
     for (void* p : wb)
       if (p) (void)hipFree(p);
     if (w.done) (void)hipEventDestroy(w.done);

@@ -203,18 +203,10 @@ __global__ __launch_bounds__(256) void k_msm_scan(const uint32_t* __restrict__ b
 // ranks from LDS atomics), then writes them out in that order: lanes of a
 // wavefront write consecutive positions of one bucket's run, so the stores
 // coalesce instead of landing as scattered 4-byte writes.  No global atomics.
-//
-// BM (block-major, batches): the block writes its LDS-sorted entries as one
-// contiguous run of SORT_BLK x W slots (every wavefront store a whole
-// 256-B span) and its local bucket starts into bcount (raddr: the block-major
-// address of run (block, bucket)); k_msm_gather then assembles bucket order
-// from line-sized pieces.  The direct form's stores land ~5 entries per
-// bucket run, a partial line each (round 3: 0.67 of its wave cycles parked
-// on memory, 1.48 ms of a 2048-MSM launch).
-template <int CB, bool BM = false>
+template <int CB>
 __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
                                                      size_t stride_words, const uint8_t* __restrict__ inf,
-                                                     uint32_t* __restrict__ bcount,
+                                                     const uint32_t* __restrict__ bcount,
                                                      const uint32_t* __restrict__ bbase, uint32_t nblk,
                                                      uint32_t* __restrict__ entries, size_t emax, uint32_t n_srs,
                                                      uint32_t point_base, uint32_t point_stride) {
@@ -279,18 +271,6 @@ __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict_
     }
   }
   __syncthreads();
-  if constexpr (BM) {
-    // entries[b][blk][0 .. total): coalesced; bcount[b][blk][k] := the
-    // block-major address of run (blk, k) (this thread read exactly these
-    // counts above)
-    uint32_t* out = entries + b * emax + (size_t)blockIdx.x * (SORT_BLK * W);
-    const uint32_t total = lstart[NB];
-    for (uint32_t j = t; j < total; j += 256) out[j] = stage[j];
-    const uint32_t base = blockIdx.x * (SORT_BLK * W);
-#pragma unroll
-    for (uint32_t j = 0; j < PER; j++) bcount[hb + t * PER + j] = base + lstart[t * PER + j];
-    return;
-  }
   for (uint32_t k = t; k < NB; k += 256) cur[k] = bbase[hb + k];  // global write bases
   __syncthreads();
 #ifdef KZGX_SCATTER_DIRECT
@@ -312,54 +292,6 @@ __global__ __launch_bounds__(256) void k_msm_scatter(const uint32_t* __restrict_
         hi = mid;
     }
     out[cur[lo] + (j - lstart[lo])] = stage[j];
-  }
-}
-
-// pass 3b (BM): bucket order from the block-major runs.  Workgroup g of MSM
-// b assembles buckets [g KB, g KB + KB): it stages, for each of its KB x nblk
-// runs (bucket-major order: bucket, then block), the run's bucket-major start
-// (bbase) and block-major address (raddr) in LDS, then every thread copies
-// positions p = off[g KB] + t, + 256, ... < off[g KB + KB] from the run that
-// holds p (binary search over the staged starts).  Both sides move
-// line-sized pieces: the KB buckets of one block are one contiguous span of
-// its run (~KB x 5 entries), and the output is one contiguous span.
-constexpr uint32_t GATHER_RUNS = 2048;  // staged runs per workgroup (<= 16 KB of LDS)
-
-template <int CB>
-__global__ __launch_bounds__(256) void k_msm_gather(const uint32_t* __restrict__ bm, size_t emax_bm,
-                                                    const uint32_t* __restrict__ raddr,
-                                                    const uint32_t* __restrict__ bbase,
-                                                    const uint32_t* __restrict__ offsets, uint32_t nblk, uint32_t KB,
-                                                    uint32_t* __restrict__ entries, size_t emax) {
-  constexpr uint32_t NB = Win<CB>::NB;
-  __shared__ uint32_t rpos[GATHER_RUNS + 1];
-  __shared__ uint32_t rsrc[GATHER_RUNS];
-  const uint32_t b = blockIdx.y;
-  const uint32_t t = threadIdx.x;
-  const uint32_t k0 = blockIdx.x * KB;
-  const uint32_t* off = offsets + (size_t)b * (NB + 1);
-  const size_t hb = (size_t)b * nblk * NB;
-  const uint32_t nr = KB * nblk;
-  for (uint32_t r = t; r < nr; r += 256) {
-    const uint32_t kk = r / nblk, blk = r - kk * nblk;
-    rpos[r] = bbase[hb + (size_t)blk * NB + k0 + kk];
-    rsrc[r] = raddr[hb + (size_t)blk * NB + k0 + kk];
-  }
-  if (t == 0) rpos[nr] = off[k0 + KB];
-  __syncthreads();
-  const uint32_t p0 = off[k0], p1 = off[k0 + KB];
-  const uint32_t* src = bm + b * emax_bm;
-  uint32_t* dst = entries + b * emax;
-  for (uint32_t p = p0 + t; p < p1; p += 256) {
-    uint32_t lo = 0, hi = nr;  // rpos[lo] <= p < rpos[hi]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (rpos[mid] <= p)
-        lo = mid;
-      else
-        hi = mid;
-    }
-    dst[p] = src[rsrc[lo] + (p - rpos[lo])];
   }
 }
 
@@ -652,72 +584,6 @@ __global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* 
   out_inf[b] = fin ? 0u : 1u;
 }
 
-// pass 5, single-call form (small batches at NB <= 1024 buckets): one
-// workgroup of NB threads per MSM, thread l holding bucket l (weight l + 1)
-// straight from bsum -- no k_msm_bucket_sums launch, no per-thread running
-// sums:  V = sum_l (l + 1) B_l = sum_l S_l,  S_l = sum_{j >= l} B_j.
-// S: a wavefront suffix scan (6 steps), then the suffix of the NB / 64
-// wavefront totals scanned by one wavefront (log2(NB / 64) steps) and added
-// back (1 step); the sum: a wavefront tree (6 steps) and a tree over the
-// wavefront sums.  The dependent chain is ~2 log2(NB) + 1 additions (19 at
-// NB = 512) against 4 + ~19 and a second launch for bucket sums + fold.
-// Lane 0 converts to affine in place.
-template <class C, uint32_t NB>
-__global__ __launch_bounds__(NB) void k_msm_fold_direct(const uint32_t* __restrict__ bsum,
-                                                        const uint32_t* __restrict__ offsets,
-                                                        uint32_t* __restrict__ xyzz_out, uint32_t* __restrict__ out,
-                                                        uint32_t* __restrict__ out_inf) {
-  constexpr int XW = xyzz_words<C>();
-  constexpr uint32_t NWV = NB / 64;
-  static_assert(NB % 64 == 0 && NWV <= 16, "one workgroup of whole wavefronts");
-  __shared__ uint32_t lds[NWV * XW];
-  const uint32_t b = blockIdx.x;
-  const uint32_t l = threadIdx.x, lane = l & 63, wv = l >> 6;
-  const uint32_t* off = offsets + (size_t)b * (NB + 1);
-  // empty buckets were never written
-  Xyzz<C> S = off[l + 1] > off[l] ? xyzz_load<C>(bsum + ((size_t)b * NB + l) * XW) : xyzz_inf<C>();
-#pragma unroll 1
-  for (int o = 1; o < 64; o <<= 1) {
-    const Xyzz<C> x = xyzz_shfl_down<C>(S, o);
-    if (lane + o < 64) S = xyzz_add_impl<C>(S, x);
-  }
-  if (lane == 0) xyzz_store<C>(lds + wv * XW, S);  // wavefront totals
-  __syncthreads();
-  if (NWV > 1 && wv == 0) {
-    // exclusive suffix sums of the totals over lanes < NWV
-    Xyzz<C> T = lane < NWV ? xyzz_load<C>(lds + lane * XW) : xyzz_inf<C>();
-#pragma unroll 1
-    for (uint32_t o = 1; o < NWV; o <<= 1) {
-      const Xyzz<C> x = xyzz_shfl_down<C>(T, (int)o);
-      if (lane + o < NWV) T = xyzz_add_impl<C>(T, x);
-    }
-    Xyzz<C> E = xyzz_shfl_down<C>(T, 1);
-    if (lane + 1 >= NWV) E = xyzz_inf<C>();
-    if (lane < NWV) xyzz_store<C>(lds + lane * XW, E);  // only this wavefront reads the totals
-  }
-  __syncthreads();
-  if (NWV > 1 && wv + 1 < NWV) S = xyzz_add_impl<C>(S, xyzz_load<C>(lds + wv * XW));
-  // V = sum of S over the workgroup
-#pragma unroll 1
-  for (int o = 32; o >= 1; o >>= 1) S = xyzz_add_impl<C>(S, xyzz_shfl_down<C>(S, o));
-  __syncthreads();  // lds is reused
-  if (lane == 0) xyzz_store<C>(lds + wv * XW, S);
-  __syncthreads();
-  if (wv != 0) return;
-  Xyzz<C> U = lane < NWV ? xyzz_load<C>(lds + lane * XW) : xyzz_inf<C>();
-#pragma unroll 1
-  for (uint32_t o = NWV / 2; o >= 1; o >>= 1) U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, (int)o));
-  if (lane != 0) return;
-  if (xyzz_out) {
-    xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
-    return;
-  }
-  Affine<C> a;
-  const bool fin = xyzz_to_affine<C>(U, a);
-  affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
-  out_inf[b] = fin ? 0u : 1u;
-}
-
 // pass 6: thread per MSM, XYZZ -> canonical affine (one inversion each), off
 // the fold's single-lane critical path
 template <class C>
@@ -879,13 +745,6 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.gmeta, batch * nwg * 2 * 4, &ws.gmeta_b));
   const bool small = batch <= KZGX_SMALL_BATCH_J;
   KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, batch * (NB / (small ? RED_J_SMALL : RED_J)) * 2 * XB, &ws.rt_b));
-  // block-major scatter + gather for batches (small batches keep the direct
-  // scatter: one launch less on the latency path); KZGX_PIP_DIRECT_SCATTER
-  // forces the direct form (A/B)
-  static const bool direct_env = std::getenv("KZGX_PIP_DIRECT_SCATTER") != nullptr;
-  const bool bm = !small && !direct_env;
-  const size_t emax_bm = nblk * (size_t)SORT_BLK * W;
-  if (bm) KZGX_TRY(dev_alloc(ctx, (void**)&ws.ebm, batch * emax_bm * 4, &ws.ebm_b));
   uint32_t* ghead = ws.gpart;
   uint32_t* gtail = ws.gpart + batch * nwg * xyzz_words<C>();
   uint32_t* gtailk = ws.gmeta;
@@ -902,22 +761,10 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
     hipLaunchKernelGGL(k_msm_scan<CB>, dim3((unsigned)batch), blk, 0, st, ws.counts, (uint32_t)nblk, ws.offsets,
                        ws.cursors);
   }
-  if (bm) {
+  {
     ProfScope p(ctx, st, "msm_scatter");
-    hipLaunchKernelGGL((k_msm_scatter<CB, true>), gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
-                       ws.counts, ws.cursors, (uint32_t)nblk, ws.ebm, emax_bm, (uint32_t)n_rows, point_base,
-                       point_stride);
-    // buckets per gather workgroup: a power of two dividing NB, at most
-    // GATHER_RUNS staged runs
-    uint32_t KB = 64;
-    while (KB > 1 && (size_t)KB * nblk > GATHER_RUNS) KB >>= 1;
-    hipLaunchKernelGGL(k_msm_gather<CB>, dim3(NB / KB, (unsigned)batch), blk, 0, st, ws.ebm, emax_bm, ws.counts,
-                       ws.cursors, ws.offsets, (uint32_t)nblk, KB, ws.entries, emax);
-  } else {
-    ProfScope p(ctx, st, "msm_scatter");
-    hipLaunchKernelGGL((k_msm_scatter<CB, false>), gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
-                       ws.counts, ws.cursors, (uint32_t)nblk, ws.entries, emax, (uint32_t)n_rows, point_base,
-                       point_stride);
+    hipLaunchKernelGGL(k_msm_scatter<CB>, gs, blk, 0, st, d_scalars, (uint32_t)n, stride_words, ctx->d_inf,
+                       ws.counts, ws.cursors, (uint32_t)nblk, ws.entries, emax, (uint32_t)n_rows, point_base, point_stride);
   }
   {
     ProfScope p(ctx, st, "msm_accum");
@@ -931,15 +778,6 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
                        ws.tailk, ws.sstate, (uint32_t)smax, NB, (uint32_t)nwg, ws.bsum, ghead, gtail, gtailk, gflag);
     hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg + 63) / 64), (unsigned)batch), dim3(64), 0, st, NB,
                        (uint32_t)nwg, ghead, gtail, gtailk, gflag, ws.bsum);
-    static const bool no_direct = std::getenv("KZGX_PIP_NO_FOLD_DIRECT") != nullptr;  // A/B
-    if constexpr (NB <= 1024) {
-      if (small && !no_direct) {
-        hipLaunchKernelGGL((k_msm_fold_direct<C, NB>), dim3((unsigned)batch), dim3(NB), 0, st, ws.bsum, ws.offsets,
-                           xyzz_out, d_out, d_out_inf);
-        KZGX_TRY_HIP(hipGetLastError());
-        return KZGX_OK;
-      }
-    }
     if (small) return bucket_reduce<C, NB, RED_J_SMALL>(ctx, ws, batch, st, d_out, d_out_inf, xyzz_out);
     return bucket_reduce<C, NB, RED_J>(ctx, ws, batch, st, d_out, d_out_inf, xyzz_out);
   }

@@ -34,6 +34,21 @@ P = np.array([[(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)] for v in 
 z0 = np.zeros((1, 4), dtype=np.uint64)
 z0[0, 0] = 12345
 print("sync_ms %.4f" % med(ctx.sync), flush=True)
+
+
+def clock_after(f):
+    """core GHz seen by a one-wave probe enqueued right after one call f():
+    the clock a single call runs at on an otherwise idle GPU"""
+    import torch
+    buf = torch.zeros(3, dtype=torch.int64, device="cuda")
+    f()
+    ctx.clock_probe(buf.data_ptr(), 200)
+    ctx.sync()
+    core, wall, khz = (int(v) for v in buf.cpu().tolist())
+    return core / wall * khz * 1e-6 if wall else None
+
+
+print("clock_ghz after a commit: %.3f" % clock_after(lambda: ctx.msm(P)), flush=True)
 for n in (1, 2, 129, 257, 1025, 4097):
     print("commit n=%5d ms %.4f   proof ms %.4f" % (n, med(lambda: ctx.msm(P[:n])),
                                                       med(lambda: ctx.prove_single_batch(P[:n], z0))), flush=True)
