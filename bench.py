@@ -637,7 +637,16 @@ def main():
                "kernel_ms_per_step": {k: v[0] / ps for k, v in pk.items()}}
     lat = None
     if not args.no_latency and args.workload != "cfg3":
-        lat = {"pippenger": latency_leg(ctx, coeffs_h)}
+        # "default": what a re-linked create_commit / create_proof runs -- the
+        # latency table (c = 8 odd multiples of the first 4097 points, built
+        # with the SRS) serves every single call of degree <= 4096;
+        # "pippenger": the same calls with it off (table-less Pippenger)
+        lt = ctx.latency_table_info()
+        lat = {"default": latency_leg(ctx, coeffs_h),
+               "default_table": {"window_bits": lt[0], "points": lt[1], "bytes": lt[2]}}
+        ctx.set_latency_table(0)
+        lat["pippenger"] = latency_leg(ctx, coeffs_h)
+        ctx.set_latency_table(lt[0], lt[1])
 
     # throughput vs table size: what a re-linked create_commit gets at each
     # HBM budget (trusted_setup::precompute_budget picks the widest window
@@ -925,6 +934,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx = kzgx.Context("BN254", device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
+    ctx.set_latency_table(0)  # one 2^20-point MSM: its HBM goes to the shard's table
     ctx.gen_srs(tau, max(count, 1), start)
     # fixed-base table over this rank's shard: the widest window whose table
     # fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB; 2^19 on 2:

@@ -107,6 +107,15 @@ int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
  * 1 = point-major.  Results are identical; only speed differs (DESIGN.md
  * section 3).  Extension with no reference counterpart. */
 int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout);
+/* the latency table (extension, no reference counterpart): odd multiples at
+ * window c over the first n_points SRS points, built with every SRS load
+ * (default c = 8 over 4097 points: 1.07 GB for BN254, 1.88 GB for
+ * BLS12-381).  Batches of at most kzgx_set_small_batch MSMs (single
+ * create_commit / create_proof calls) that fit in it take its two-launch
+ * path; everything else is unchanged.  c = 0 turns it off (single calls then
+ * run the table-less Pippenger).  Rebuilt at once when an SRS is installed. */
+int kzgx_set_latency_table(kzgx_ctx* ctx, int c, size_t n_points);
+int kzgx_latency_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
 /* layout of the built table: *point_major = 1 (M[i][w][j]) or 0 (M[w][i][j]) */
 int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major);
 /* built table: window bits (0 = none), points covered, device bytes */

@@ -98,6 +98,15 @@ struct ProfRec {
   hipEvent_t a, b;
 };
 
+// the default latency table (Ctx::fixed_lat): c = 8 odd multiples of the
+// first 4097 SRS points -- degree-4096 calls and below, 1.07 GB for BN254
+#ifndef KZGX_LAT_TABLE_BITS
+#define KZGX_LAT_TABLE_BITS 8
+#endif
+#ifndef KZGX_LAT_TABLE_POINTS
+#define KZGX_LAT_TABLE_POINTS 4097
+#endif
+
 // batches of at most this many MSMs use the small-window table (msm.hip)
 #ifndef KZGX_SMALL_BATCH
 #define KZGX_SMALL_BATCH 16
@@ -123,6 +132,11 @@ struct Ctx {
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];
   FixedTable fixed;
+  // the latency table: odd multiples at a small window over the first SRS
+  // points, built with the SRS by default and read only by small batches
+  // (single create_commit / create_proof calls) that the main table does not
+  // serve (msm.hip msm_batch; kzgx_set_latency_table)
+  FixedTable fixed_lat{KZGX_LAT_TABLE_BITS, KZGX_LAT_TABLE_POINTS};
   // the workspace bound to stream st (claimed on first use; every lookup
   // refreshes its use stamp).  With more than KZGX_MAX_STREAMS distinct
   // streams the least recently USED slot is rebound once the work of its
@@ -211,9 +225,14 @@ int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap);
 bool window_bits_supported(int c);
 bool fixed_bits_supported(int c);
 int fixed_windows(int curve, int c);
-int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);
-void fixed_free(Ctx* ctx);
+int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);  // the main and the latency table
+int fixed_build_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t n_srs);
+void fixed_free(Ctx* ctx);  // the main table
+void fixed_free_table(FixedTable& ft);
 bool fixed_usable(const Ctx* ctx, size_t n);
+bool fixed_table_usable(const FixedTable& ft, size_t n);
+int fixed_msm_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                    uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out);
 int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out);
 int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);

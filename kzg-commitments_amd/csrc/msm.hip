@@ -861,6 +861,11 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;
   if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
+  // single calls and small batches inside the latency table's prefix: the
+  // table's two-launch latency path (k_fixed_accum_lat) instead of eight
+  // Pippenger launches whose bucket reduction is a ~20-addition chain
+  if (batch <= ctx->small_batch && fixed_table_usable(ctx->fixed_lat, n))
+    return fixed_msm_table(ctx, ctx->fixed_lat, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
 // Single MSMs chunk from 2^17 points: below, one un-chunked Pippenger (the
 // segment length shrinks to spread it) has one reduction level less; above,
 // its one-workgroup scan over n / 512 count blocks serialises (measured,

@@ -374,8 +374,7 @@ static TabStrides tab_strides(const FixedTable& ft) {
 static const uint8_t* fixed_inf(const FixedTable& ft) { return ft.any_inf ? ft.inf : nullptr; }
 
 template <class C>
-static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
-  FixedTable& ft = ctx->fixed;
+static int fixed_build_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t n) {
   const int c = ft.c_req;
   const int W = fixed_windows(ctx->curve, c);
   const uint64_t H = 1ull << (c - 1);
@@ -385,11 +384,11 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   // most of the device
   if (ft.d || ft.inf) {
     KZGX_TRY_HIP(hipDeviceSynchronize());
-    fixed_free(ctx);
+    fixed_free_table(ft);
   }
   // any failure below leaves no table (and no half-built allocation) behind
   struct Guard {
-    Ctx* ctx;
+    FixedTable& ft;
     uint32_t* bases = nullptr;
     uint8_t* inf = nullptr;
     bool ok = false;
@@ -397,10 +396,10 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
       if (bases) (void)hipFree(bases);
       if (!ok) {
         if (inf) (void)hipFree(inf);
-        fixed_free(ctx);
+        fixed_free_table(ft);
       }
     }
-  } g{ctx};
+  } g{ft};
   KZGX_TRY_HIP(hipMalloc((void**)&ft.d, bytes));
   ft.bytes = bytes;
   KZGX_TRY_HIP(hipMalloc((void**)&g.bases, (size_t)W * n * PB));
@@ -446,16 +445,21 @@ static int fixed_build_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   return KZGX_OK;
 }
 
-int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
-  FixedTable& ft = ctx->fixed;
+int fixed_build_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t n_srs) {
   if (ft.c_req == 0 || ft.n_req == 0) return KZGX_OK;
   const size_t n = ft.n_req < n_srs ? ft.n_req : n_srs;
-  return ctx->curve == KZGX_CURVE_BN254 ? fixed_build_impl<BN254G1>(ctx, d_canon, n)
-                                        : fixed_build_impl<BLS12381G1>(ctx, d_canon, n);
+  return ctx->curve == KZGX_CURVE_BN254 ? fixed_build_impl<BN254G1>(ctx, ft, d_canon, n)
+                                        : fixed_build_impl<BLS12381G1>(ctx, ft, d_canon, n);
 }
 
-void fixed_free(Ctx* ctx) {
-  FixedTable& ft = ctx->fixed;
+int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
+  KZGX_TRY(fixed_build_table(ctx, ctx->fixed, d_canon, n_srs));
+  return fixed_build_table(ctx, ctx->fixed_lat, d_canon, n_srs);
+}
+
+void fixed_free(Ctx* ctx) { fixed_free_table(ctx->fixed); }
+
+void fixed_free_table(FixedTable& ft) {
   if (ft.d) (void)hipFree(ft.d);
   if (ft.inf) (void)hipFree(ft.inf);
   ft.d = nullptr;
@@ -467,9 +471,9 @@ void fixed_free(Ctx* ctx) {
 }
 
 template <class C, int CB>
-static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
-                          uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
-  FixedTable& ft = ctx->fixed;
+static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n, size_t batch,
+                          size_t stride_words, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st,
+                          uint32_t* xyzz_out) {
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
   // latency path: a few MSMs of <= 2^14 points (k_fixed_accum_lat)
   static const bool lat_off = std::getenv("KZGX_NO_FIXED_LAT") != nullptr;
@@ -595,11 +599,11 @@ static int fixed_msm_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t 
 }
 
 template <class C>
-static int fixed_msm_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
-                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
-  switch (ctx->fixed.c) {
+static int fixed_msm_c(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n, size_t batch,
+                       size_t stride_words, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  switch (ft.c) {
 #define KZGX_FIXED_CASE(cb) \
-  case cb: return fixed_msm_impl<C, cb>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
+  case cb: return fixed_msm_impl<C, cb>(ctx, ft, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
     KZGX_FIXED_CASE(4)
     KZGX_FIXED_CASE(7)
     KZGX_FIXED_CASE(8)
@@ -629,15 +633,21 @@ bool fixed_bits_supported(int c) {
 
 // (a prefix of infinite points only -- a loaded all-infinity SRS -- has no
 // finite point to carry the identity terms of k_fixed_accum: Pippenger)
-bool fixed_usable(const Ctx* ctx, size_t n) {
-  return ctx->fixed.d && ctx->fixed.n_t > 0 && n <= ctx->fixed.n_t && ctx->fixed.fin0 != UINT32_MAX;
+bool fixed_table_usable(const FixedTable& ft, size_t n) {
+  return ft.d && ft.n_t > 0 && n <= ft.n_t && ft.fin0 != UINT32_MAX;
+}
+bool fixed_usable(const Ctx* ctx, size_t n) { return fixed_table_usable(ctx->fixed, n); }
+
+int fixed_msm_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                    uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  return ctx->curve == KZGX_CURVE_BN254
+             ? fixed_msm_c<BN254G1>(ctx, ft, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out)
+             : fixed_msm_c<BLS12381G1>(ctx, ft, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
 }
 
 int fixed_msm(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
-  return ctx->curve == KZGX_CURVE_BN254
-             ? fixed_msm_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out)
-             : fixed_msm_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
+  return fixed_msm_table(ctx, ctx->fixed, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, xyzz_out);
 }
 
 // --------------------------------------------------------------------------

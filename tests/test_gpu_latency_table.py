@@ -1,0 +1,117 @@
+"""The default latency table (kzgx_set_latency_table, Ctx::fixed_lat): odd
+multiples at c = 8 over the first 4097 SRS points, built with the SRS, read
+by batches of <= 16 MSMs that fit in it -- every single create_commit /
+create_proof of degree <= 4096 (the reference's benchmark calls,
+benchmark/benchmark.cpp:40-66).  Checked against the known-tau identity
+commit = [P(tau)]G1 / proof = [q(tau)]G1 (oracle), at the sizes around the
+table's edges, on both curves, with a degenerate SRS, and with the table off
+or too short (Pippenger)."""
+import numpy as np
+import pytest
+
+import kzg_ref as K
+
+pytestmark = pytest.mark.gpu
+
+CURVES = [("BN254", K.BN254), ("BLS12381", K.BLS12381)]
+
+
+def limbs(vals, nl=4):
+    import corc
+    return corc.ints_to_limbs(vals, nl)
+
+
+def pt(curve, row, inf=False):
+    import corc
+    return None if inf else corc.array_to_points(curve, row[None, :])[0]
+
+
+@pytest.fixture(scope="module")
+def lat_ctx():
+    import kzgx
+    made = {}
+
+    def get(name, C):
+        if name not in made:
+            ctx = kzgx.Context(name)
+            ctx.gen_srs(K.default_tau(C), 4200)
+            made[name] = ctx
+        return made[name]
+
+    yield get
+    for c in made.values():
+        c.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_latency_table_is_built_by_default(name, C, lat_ctx):
+    import kzgx
+    ctx = lat_ctx(name, C)
+    c, n, b = ctx.latency_table_info()
+    assert (c, n) == (8, 4097)
+    assert b == kzgx.fixed_base_bytes(name, 8, 4097)
+    assert ctx.fixed_base_info()[0] == 0  # the main (throughput) table stays opt-in
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n", [1, 2, 129, 4096, 4097, 4098])
+def test_single_commit_matches_oracle(name, C, n, lat_ctx):
+    """n <= 4097: the latency table; 4098: past its prefix (Pippenger)"""
+    ctx = lat_ctx(name, C)
+    tau = K.default_tau(C)
+    P = K.random_scalars(C, n, seed=7100 + n)
+    if n >= 3:
+        P[0], P[1], P[-1] = 0, C.r - 1, 2
+    out, inf = ctx.msm(limbs(P))
+    assert pt(name, out, inf) == K.commit_via_tau(C, tau, P)
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("batch", [2, 16, 17])
+def test_small_batches(name, C, batch, lat_ctx):
+    """<= 16 MSMs take the table, 17 the batched Pippenger"""
+    ctx = lat_ctx(name, C)
+    tau = K.default_tau(C)
+    n = 300
+    polys = [K.random_scalars(C, n, seed=7300 + b) for b in range(batch)]
+    polys[0] = [0] * n  # the zero polynomial -> infinity
+    out, inf = ctx.msm_batch(np.concatenate([limbs(P) for P in polys]), n, batch)
+    for b in range(batch):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_single_proofs(name, C, lat_ctx):
+    """create_proof(poly, z, 1) at degree 128 and 4096: quotient + table MSM"""
+    ctx = lat_ctx(name, C)
+    tau = K.default_tau(C)
+    for n in (129, 4097):
+        P = K.random_scalars(C, n, seed=7500 + n)
+        z = 12345 + n
+        zs = np.array([[z, 0, 0, 0]], dtype=np.uint64)
+        out, inf, y = ctx.prove_single_batch(limbs(P), zs)
+        assert pt(name, out[0], inf[0]) == K.commit_via_tau(C, tau, K.proof_quotient(C, P, z, 1))
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_latency_table_off_and_degenerate(name, C):
+    """c = 0 turns it off (Pippenger); tau = 0 (every SRS point but the
+    first infinite) still exact through the table"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(0, 200)
+        assert ctx.latency_table_info()[:2] == (8, 200)
+        P = K.random_scalars(C, 150, seed=7700)
+        out, inf = ctx.msm(limbs(P))
+        assert pt(name, out, inf) == K.commit_via_tau(C, 0, P)
+        ctx.set_latency_table(0)
+        assert ctx.latency_table_info() == (0, 0, 0)
+        out2, inf2 = ctx.msm(limbs(P))
+        assert pt(name, out2, inf2) == K.commit_via_tau(C, 0, P)
+        ctx.set_latency_table(7, 100)  # rebuilt at once over the installed SRS
+        assert ctx.latency_table_info()[:2] == (7, 100)
+        out3, inf3 = ctx.msm(limbs(P[:90]))
+        assert pt(name, out3, inf3) == K.commit_via_tau(C, 0, P[:90])
+    finally:
+        ctx.close()
