@@ -619,6 +619,10 @@ void trusted_setup::precompute(int window_bits, size_t points) {
         "kzgx_set_fixed_base");
 }
 
+void trusted_setup::latency_table(int window_bits, size_t points) {
+  check(kzgx_set_latency_table(ctx, window_bits, window_bits ? points : 0), "kzgx_set_latency_table");
+}
+
 int trusted_setup::precompute_budget(size_t budget_bytes, size_t points) {
   int c = 0;
   check(kzgx_set_fixed_base_budget(ctx, budget_bytes, points ? std::min(points, n) : n, &c),

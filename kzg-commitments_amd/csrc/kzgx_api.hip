@@ -213,7 +213,8 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   kzgx::fixed_free_table(c.fixed_lat);
   for (auto& w : c.ws) {
     void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
-                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig};
+                  w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig,
+                  w.lat_cnt};
     for (void* p : wb)
       if (p) (void)hipFree(p);
     if (w.done) (void)hipEventDestroy(w.done);

@@ -41,6 +41,7 @@ struct MsmWs {
   uint32_t *bsum = nullptr, *heads = nullptr, *tails = nullptr, *tailk = nullptr, *rt = nullptr, *q = nullptr,
            *parts = nullptr, *fpart = nullptr, *fsum = nullptr, *gpart = nullptr, *gmeta = nullptr, *qbig = nullptr;
   uint8_t* sstate = nullptr;
+  uint32_t* lat_cnt = nullptr;  // [64] arrival counters of the one-launch latency path (msm_fixed.hip)
   size_t counts_b = 0, offsets_b = 0, cursors_b = 0, entries_b = 0, bsum_b = 0, heads_b = 0, tails_b = 0, tailk_b = 0,
          rt_b = 0, q_b = 0, parts_b = 0, fpart_b = 0, fsum_b = 0, gpart_b = 0, gmeta_b = 0, sstate_b = 0, qbig_b = 0;
   hipStream_t owner = nullptr;  // workspaces are per stream so calls on

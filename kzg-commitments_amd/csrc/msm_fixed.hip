@@ -173,6 +173,10 @@ KZGX_DEV Xyzz<C> xyzz_shfl_xor_add(const Xyzz<C>& acc, int off) {
   return xyzz_add_impl<C>(acc, o);
 }
 
+template <class C>
+KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
+                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf);
+
 // thread (g, i): point i < n_pad of MSM b, windows [g WG, min(W, (g + 1) WG));
 // wavefront partial q = (g n_pad + i) / 64 -> part[b][q]
 template <class C, int CB>
@@ -180,7 +184,8 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
                                                         uint32_t n_pad, size_t stride_words,
                                                         const uint32_t* __restrict__ tab, TabStrides ts,
                                                         const uint8_t* __restrict__ inf, int WG, uint32_t Q,
-                                                        uint32_t* __restrict__ part) {
+                                                        uint32_t* __restrict__ part, uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
@@ -215,16 +220,29 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
   }
 #pragma unroll 1
   for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
-  if (threadIdx.x == 0) xyzz_store<C>(part + ((size_t)b * Q + t / 64) * XW, acc);
+  // the last of MSM b's Q wavefronts to finish folds the Q partials (one
+  // launch per call instead of two): release the partial, count it in
+  // (device-scope atomic), and the wavefront that counts the Q-th acquires
+  // the others and runs the fold
+  uint32_t prev = 0;
+  if (threadIdx.x == 0) {
+    xyzz_store<C>(part + ((size_t)b * Q + t / 64) * XW, acc);
+    __threadfence();
+    prev = atomicAdd(cnt + b, 1u);
+  }
+  prev = __shfl(prev, 0, 64);
+  if (prev + 1 != Q) return;
+  __threadfence();
+  lat_fold_finish<C>(part, Q, b, threadIdx.x, out, out_inf);
+  if (threadIdx.x == 0) cnt[b] = 0;  // ready for the next call (stream order)
 }
 
-// one wavefront per MSM: lane sums partials lane, lane + 64, ... < Q, a
-// shuffle tree over the lanes that hold any, lane 0 converts and stores
+// MSM b's fold by one wavefront: lane sums partials lane, lane + 64, ... <
+// Q, a shuffle tree over the lanes that hold any, lane 0 converts and stores
 template <class C>
-__global__ __launch_bounds__(64) void k_fixed_fold_finish(const uint32_t* __restrict__ part, uint32_t Q,
-                                                          uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
+                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
   constexpr int XW = xyzz_words<C>();
-  const uint32_t b = blockIdx.x, lane = threadIdx.x;
   const uint32_t* p = part + (size_t)b * Q * XW;
   Xyzz<C> acc = lane < Q ? xyzz_load<C>(p + (size_t)lane * XW) : xyzz_inf<C>();
 #pragma unroll 1
@@ -490,11 +508,14 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
     WsLease wsp = ctx->ws_for(st);
     if (!wsp) return KZGX_ERR_ARG;
     KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
+    if (!wsp->lat_cnt) {  // per-MSM arrival counters, zero between calls
+      KZGX_TRY_HIP(hipMalloc((void**)&wsp->lat_cnt, 64 * sizeof(uint32_t)));
+      KZGX_TRY_HIP(hipMemsetAsync(wsp->lat_cnt, 0, 64 * sizeof(uint32_t), st));
+    }
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
-                       (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), WG, Q, wsp->fpart);
-    hipLaunchKernelGGL(k_fixed_fold_finish<C>, dim3((unsigned)batch), dim3(64), 0, st, wsp->fpart, Q, d_out,
-                       d_out_inf);
+                       (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), WG, Q, wsp->fpart,
+                       wsp->lat_cnt, d_out, d_out_inf);
     KZGX_TRY_HIP(hipGetLastError());
     return KZGX_OK;
   }
