@@ -626,27 +626,31 @@ def main():
     # 255-bit scalars need 16 windows at either width
     fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else shape["fixed_bits"]
 
-    # ---- secondary legs on the default product path (no table): what
-    # kzg::trusted_setup::create_commit / create_proof do without precompute()
-    pip = None
-    if fixed_bits and not args.no_pippenger:
-        pe, pk, _ = timed_run(ctx, step, streams, max(3, min(args.steps, 6)), 1, world, dist, torch, dev)
-        ps = max(3, min(args.steps, 6))
-        pip = {"value": units_all * ps / pe, "ms_per_step": pe / ps * 1e3,
-               "msm": "pippenger, c=%d, segment %d" % (args.window_bits, args.segment),
-               "kernel_ms_per_step": {k: v[0] / ps for k, v in pk.items()}}
-    lat = None
+    # ---- secondary legs on the product paths without precompute(): what
+    # kzg::trusted_setup::create_commit / create_proof run out of the box
+    # ("default": the budget-chosen default table of the first 4097 SRS
+    # points, built with the SRS) and with that table off ("pippenger": the
+    # table-less path, which allocates nothing beyond the SRS like the
+    # reference, src/trusted_setup.cpp:137-142)
+    dt = ctx.default_table_info()
+    dflt = pip = lat = None
+    sec_steps = max(3, min(args.steps, 6))
+    if fixed_bits and not args.no_pippenger and dt[0]:
+        de, dk, _ = timed_run(ctx, step, streams, sec_steps, 1, world, dist, torch, dev)
+        dflt = {"value": units_all * sec_steps / de, "ms_per_step": de / sec_steps * 1e3,
+                "msm": "default table, c=%d over %d points (%.2f GB)" % (dt[0], dt[1], dt[2] / 1e9),
+                "kernel_ms_per_step": {k: v[0] / sec_steps for k, v in dk.items()}}
     if not args.no_latency and args.workload != "cfg3":
-        # "default": what a re-linked create_commit / create_proof runs -- the
-        # latency table (c = 8 odd multiples of the first 4097 points, built
-        # with the SRS) serves every single call of degree <= 4096;
-        # "pippenger": the same calls with it off (table-less Pippenger)
-        lt = ctx.latency_table_info()
         lat = {"default": latency_leg(ctx, coeffs_h),
-               "default_table": {"window_bits": lt[0], "points": lt[1], "bytes": lt[2]}}
-        ctx.set_latency_table(0)
+               "default_table": {"window_bits": dt[0], "points": dt[1], "bytes": dt[2]}}
+    ctx.set_default_table(0)  # off from here on: the main table serves the rest
+    if fixed_bits and not args.no_pippenger:
+        pe, pk, _ = timed_run(ctx, step, streams, sec_steps, 1, world, dist, torch, dev)
+        pip = {"value": units_all * sec_steps / pe, "ms_per_step": pe / sec_steps * 1e3,
+               "msm": "pippenger, c=%d, segment %d" % (args.window_bits, args.segment),
+               "kernel_ms_per_step": {k: v[0] / sec_steps for k, v in pk.items()}}
+    if lat is not None:
         lat["pippenger"] = latency_leg(ctx, coeffs_h)
-        ctx.set_latency_table(lt[0], lt[1])
 
     # throughput vs table size: what a re-linked create_commit gets at each
     # HBM budget (trusted_setup::precompute_budget picks the widest window
@@ -895,6 +899,7 @@ def main():
                                  "partial product is)",
                 },
                 "table_curve": curve_pts,
+                "default_table": dflt,
                 "pippenger": pip,
                 "latency": lat,
                 "setup_ms": setup,
@@ -934,7 +939,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx = kzgx.Context("BN254", device=local)
     ctx.set_window_bits(args.window_bits)
     ctx.set_segment(args.segment)
-    ctx.set_latency_table(0)  # one 2^20-point MSM: its HBM goes to the shard's table
+    ctx.set_default_table(0)  # one 2^20-point MSM: its HBM goes to the shard's table
     ctx.gen_srs(tau, max(count, 1), start)
     # fixed-base table over this rank's shard: the widest window whose table
     # fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB; 2^19 on 2:

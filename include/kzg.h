@@ -192,17 +192,17 @@ class trusted_setup {
    *  257.8 GB of HBM, c = 16 137.5 GB, c = 12 11.8 GB, and BLS12-381 c = 16
    *  240.6 GB.  Commits and proofs over that prefix then run as plain table
    *  sums.  window_bits = 0 drops the table.  Without it, batches run on
-   *  Pippenger and single calls on the latency table below. */
+   *  the default table below. */
   void precompute(int window_bits = 16, size_t points = 0);
-  /** Extension: the latency table (kzgx_set_latency_table), built with every
-   *  setup by default: c = 8 odd multiples of the first 4097 SRS points
-   *  (1.07 GB BN254 / 1.88 GB BLS12-381).  Single create_commit /
-   *  create_proof calls of degree <= 4096 take its one-launch path (degree
-   *  128: 0.41 -> 0.15 ms, degree 4096: 0.50 -> 0.23 ms on MI355X).  The
-   *  reference's create_commit allocates nothing beyond the SRS
-   *  (src/trusted_setup.cpp:137-142): latency_table(0) restores that, and
-   *  single calls then run the table-less Pippenger. */
-  void latency_table(int window_bits, size_t points = 4097);
+  /** Extension: the default table (kzgx_set_default_table), built with
+   *  every setup: odd multiples of the first 4097 SRS points at the widest
+   *  window c <= 12 that fits 2.5% of the HBM (window_bits = -1, the default:
+   *  BN254 c = 11, 6.4 GB; BLS12-381 c = 10, 6.1 GB).  Single create_commit /
+   *  create_proof calls of degree <= 4096 take its one-launch path, batches
+   *  its batched kernel.  The reference's create_commit allocates nothing
+   *  beyond the SRS (src/trusted_setup.cpp:137-142): default_table(0)
+   *  restores that, and every MSM then runs the table-less Pippenger. */
+  void default_table(int window_bits, size_t points = 4097);
   /** Extension: the widest window whose table over `points` SRS points
    *  (0 = all) fits `budget_bytes` and the free HBM; returns the window
    *  built (0: none fits, Pippenger stays).  DESIGN.md section 3 holds the

@@ -107,15 +107,21 @@ int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
  * 1 = point-major.  Results are identical; only speed differs (DESIGN.md
  * section 3).  Extension with no reference counterpart. */
 int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout);
-/* the latency table (extension, no reference counterpart): odd multiples at
- * window c over the first n_points SRS points, built with every SRS load
- * (default c = 8 over 4097 points: 1.07 GB for BN254, 1.88 GB for
- * BLS12-381).  Batches of at most kzgx_set_small_batch MSMs (single
- * create_commit / create_proof calls) that fit in it take its two-launch
- * path; everything else is unchanged.  c = 0 turns it off (single calls then
- * run the table-less Pippenger).  Rebuilt at once when an SRS is installed. */
-int kzgx_set_latency_table(kzgx_ctx* ctx, int c, size_t n_points);
-int kzgx_latency_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
+/* the default table (extension, no reference counterpart): odd multiples at
+ * window c over the first n_points SRS points, built with every SRS load.
+ * c = -1 (the default) picks the widest c <= 12 whose table fits 2.5% of the
+ * device memory and its free memory less 4 GiB: over 4097 points BN254
+ * c = 11 (6.4 GB), BLS12-381 c = 10 (6.1 GB) on an MI355X.  MSMs that fit in
+ * it and that the main table (kzgx_set_fixed_base) does not serve take it:
+ * batches of at most kzgx_set_small_batch MSMs (single create_commit /
+ * create_proof calls) its one-launch path, larger batches its batched
+ * kernel when c >= 10 (BN254) / 11 (BLS12-381), below which the batched
+ * Pippenger is as fast.  c = 0 turns it off (every such MSM then runs the
+ * table-less Pippenger, as the reference allocates nothing beyond the SRS);
+ * c in {4, 7..17} fixes the window.  Rebuilt at once when an SRS is
+ * installed. */
+int kzgx_set_default_table(kzgx_ctx* ctx, int c, size_t n_points);
+int kzgx_default_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
 /* layout of the built table: *point_major = 1 (M[i][w][j]) or 0 (M[w][i][j]) */
 int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major);
 /* built table: window bits (0 = none), points covered, device bytes */

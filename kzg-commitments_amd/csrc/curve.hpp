@@ -375,7 +375,9 @@ KZGX_DEV Xyzz<C> xyzz_add_impl(const Xyzz<C>& p, const Xyzz<C>& q) {
 }
 
 // XYZZ -> affine, canonical Montgomery (< m).  Returns false for infinity.
-template <class C>
+// UNIFORM: one lane's conversion (the first active lane's point), its
+// inversion on the scalar ALU (f29_inv_uniform)
+template <class C, bool UNIFORM = false>
 KZGX_DEV bool xyzz_to_affine_impl(const Xyzz<C>& p, Affine<C>& out) {
   using F = typename C::Fp29;
   if (xyzz_is_inf<C>(p)) {
@@ -384,7 +386,9 @@ KZGX_DEV bool xyzz_to_affine_impl(const Xyzz<C>& p, Affine<C>& out) {
     return false;
   }
   F29<F> t = f29_mul<F>(p.ZZ, p.ZZZ);
-  F29<F> i = f29_inv_fast<F, C::Fp::N>(t, C::Fp::P, C::Fp::PM2);  // 1 / (ZZ ZZZ)
+  F29<F> i;  // 1 / (ZZ ZZZ)
+  if constexpr (UNIFORM) i = f29_inv_uniform<F, C::Fp::N>(t, C::Fp::P);
+  else i = f29_inv_fast<F, C::Fp::N>(t, C::Fp::P, C::Fp::PM2);
   F29<F> izz = f29_mul<F>(i, p.ZZZ);               // 1 / ZZ
   F29<F> izzz = f29_mul<F>(i, p.ZZ);               // 1 / ZZZ
   out.x = f29_reduce<F>(f29_mul<F>(p.X, izz));
@@ -432,6 +436,13 @@ KZGX_PT Xyzz<C> xyzz_add(const Xyzz<C>& p, const Xyzz<C>& q) {
 template <class C>
 KZGX_PT bool xyzz_to_affine(const Xyzz<C>& p, Affine<C>& out) {
   return xyzz_to_affine_impl<C>(p, out);
+}
+
+// one lane's conversion (only the calling lane active, or every active lane
+// holding the same point)
+template <class C>
+KZGX_PT bool xyzz_to_affine_lane(const Xyzz<C>& p, Affine<C>& out) {
+  return xyzz_to_affine_impl<C, true>(p, out);
 }
 
 // ---- storage ---------------------------------------------------------------

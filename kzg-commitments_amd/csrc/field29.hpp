@@ -849,10 +849,22 @@ __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW
 // 13 passes on average (16 at most over 3000 random inputs), BLS12-381 19
 // (21).  The Montgomery form of the result, (y / R)^-1 R = v R^2, is two
 // products by R^2 mod m.
-template <class F, int NW>
-__device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in, const uint32_t (&)[NW]) {
+//
+// U (wave-uniform): the caller guarantees the first active lane holds the
+// value every lane needs -- a single lane's tail (lane 0 of the latency
+// path's fold) -- and the input is read from that lane, so the whole GCD
+// state is uniform and runs on the scalar ALU: one SALU instruction per
+// clock where a lone wave's dependent VALU instruction costs ~8.  Never with
+// a different value per lane (the batched finish kernels).
+template <class F, int NW, bool U = false>
+__device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[NW]) {
   constexpr int L = F::L;
   constexpr int K = 29;
+  F29<F> in = in_;
+  if constexpr (U) {
+#pragma unroll
+    for (int j = 0; j < L; j++) in.v[j] = __builtin_amdgcn_readfirstlane(in.v[j]);
+  }
   F29<F> a = f29_reduce<F>(in), b = f29_const<F>(F::P), u = f29_zero<F>(), v = f29_zero<F>();
   if (f29_is_zero_exact<F>(a)) return a;
   u.v[0] = 1;
@@ -976,6 +988,12 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in, const uint32_t (&)[N
   }
   const F29<F> r2 = f29_const<F>(F::R2);
   return f29_mul<F>(f29_mul<F>(v, r2), r2);
+}
+
+// a^-1 of the first active lane's a (see U above)
+template <class F, int NW>
+KZGX_DEV F29<F> f29_inv_uniform(const F29<F>& a, const uint32_t (&m)[NW]) {
+  return f29_inv_vt<F, NW, true>(a, m);
 }
 
 // the inversion the finish / pairing paths use (KZGX_INV_FERMAT: the

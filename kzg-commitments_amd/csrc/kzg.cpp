@@ -619,8 +619,8 @@ void trusted_setup::precompute(int window_bits, size_t points) {
         "kzgx_set_fixed_base");
 }
 
-void trusted_setup::latency_table(int window_bits, size_t points) {
-  check(kzgx_set_latency_table(ctx, window_bits, window_bits ? points : 0), "kzgx_set_latency_table");
+void trusted_setup::default_table(int window_bits, size_t points) {
+  check(kzgx_set_default_table(ctx, window_bits, window_bits ? points : 0), "kzgx_set_default_table");
 }
 
 int trusted_setup::precompute_budget(size_t budget_bytes, size_t points) {

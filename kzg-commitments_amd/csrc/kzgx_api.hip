@@ -210,7 +210,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   kzgx::fixed_free(&c);
-  kzgx::fixed_free_table(c.fixed_lat);
+  kzgx::fixed_free_table(c.fixed_def);
   for (auto& w : c.ws) {
     void* wb[] = {w.counts, w.offsets, w.cursors, w.entries, w.bsum,  w.heads,
                   w.tails,  w.tailk,   w.rt,      w.q,       w.parts, w.fpart, w.fsum, w.gpart, w.gmeta, w.sstate, w.qbig,
@@ -305,28 +305,28 @@ int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points) {
   kzgx::fixed_free(&ctx->c);
   ctx->c.fixed.c_req = c;
   ctx->c.fixed.n_req = c ? n_points : 0;
-  if (c != 0 && ctx->c.n_srs != 0) KZGX_TRY(kzgx::fixed_build(&ctx->c, ctx->d_srs_canon, ctx->c.n_srs));
+  if (c != 0 && ctx->c.n_srs != 0)
+    KZGX_TRY(kzgx::fixed_build_table(&ctx->c, ctx->c.fixed, ctx->d_srs_canon, ctx->c.n_srs));  // the default table stays
   return KZGX_OK;
 }
 
-int kzgx_set_latency_table(kzgx_ctx* ctx, int c, size_t n_points) {
+int kzgx_set_default_table(kzgx_ctx* ctx, int c, size_t n_points) {
   KZGX_TRY(activate(ctx));
-  if (!kzgx::fixed_bits_supported(c)) return KZGX_ERR_ARG;
+  if (c != -1 && !kzgx::fixed_bits_supported(c)) return KZGX_ERR_ARG;
   if (c != 0 && n_points == 0) return KZGX_ERR_ARG;
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
-  kzgx::fixed_free_table(ctx->c.fixed_lat);
-  ctx->c.fixed_lat.c_req = c;
-  ctx->c.fixed_lat.n_req = c ? n_points : 0;
-  if (c != 0 && ctx->c.n_srs != 0)
-    KZGX_TRY(kzgx::fixed_build_table(&ctx->c, ctx->c.fixed_lat, ctx->d_srs_canon, ctx->c.n_srs));
+  kzgx::fixed_free_table(ctx->c.fixed_def);
+  ctx->c.fixed_def.c_req = c;
+  ctx->c.fixed_def.n_req = c ? n_points : 0;
+  if (c != 0 && ctx->c.n_srs != 0) KZGX_TRY(kzgx::fixed_rebuild_default(&ctx->c, ctx->d_srs_canon, ctx->c.n_srs));
   return KZGX_OK;
 }
 
-int kzgx_latency_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes) {
+int kzgx_default_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes) {
   if (!ctx) return KZGX_ERR_ARG;
-  if (c) *c = ctx->c.fixed_lat.c;
-  if (n_points) *n_points = ctx->c.fixed_lat.n_t;
-  if (bytes) *bytes = ctx->c.fixed_lat.bytes;
+  if (c) *c = ctx->c.fixed_def.c;
+  if (n_points) *n_points = ctx->c.fixed_def.n_t;
+  if (bytes) *bytes = ctx->c.fixed_def.bytes;
   return KZGX_OK;
 }
 

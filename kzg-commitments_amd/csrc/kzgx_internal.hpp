@@ -99,13 +99,30 @@ struct ProfRec {
   hipEvent_t a, b;
 };
 
-// the default latency table (Ctx::fixed_lat): c = 8 odd multiples of the
-// first 4097 SRS points -- degree-4096 calls and below, 1.07 GB for BN254
-#ifndef KZGX_LAT_TABLE_BITS
-#define KZGX_LAT_TABLE_BITS 8
+// the default table (Ctx::fixed_def): odd multiples of the first 4097 SRS
+// points (degree-4096 calls and below) at the widest window c <= 12 whose
+// table fits KZGX_DEFAULT_TABLE_PERMILLE of the device's memory -- 25 per
+// mille = 7.2 GB of an MI355X: BN254 c = 11 (6.4 GB), BLS12-381 c = 10
+// (6.1 GB).  -1 = that automatic choice, 0 = none, c = a fixed window.
+#ifndef KZGX_DEFAULT_TABLE_BITS
+#define KZGX_DEFAULT_TABLE_BITS -1
 #endif
-#ifndef KZGX_LAT_TABLE_POINTS
-#define KZGX_LAT_TABLE_POINTS 4097
+#ifndef KZGX_DEFAULT_TABLE_POINTS
+#define KZGX_DEFAULT_TABLE_POINTS 4097
+#endif
+#ifndef KZGX_DEFAULT_TABLE_PERMILLE
+#define KZGX_DEFAULT_TABLE_PERMILLE 25
+#endif
+// batches larger than Ctx::small_batch use the default table from this
+// window on (below it the batched Pippenger is as fast or faster).  cfg2
+// shape, BN254: c = 10 138k-141k / 11 148k-151k / 12 161k-164k against
+// Pippenger's 130k per second; cfg4 shape, BLS12-381: c = 10 63k-64k /
+// 12 75k against 64k (profiles/r04_default_table_windows.json)
+#ifndef KZGX_DEFAULT_TABLE_BATCH_MIN_C_BN
+#define KZGX_DEFAULT_TABLE_BATCH_MIN_C_BN 10
+#endif
+#ifndef KZGX_DEFAULT_TABLE_BATCH_MIN_C_BLS
+#define KZGX_DEFAULT_TABLE_BATCH_MIN_C_BLS 11
 #endif
 
 // batches of at most this many MSMs use the small-window table (msm.hip)
@@ -133,11 +150,11 @@ struct Ctx {
   size_t inf_bytes = 0;
   MsmWs ws[KZGX_MAX_STREAMS];
   FixedTable fixed;
-  // the latency table: odd multiples at a small window over the first SRS
-  // points, built with the SRS by default and read only by small batches
-  // (single create_commit / create_proof calls) that the main table does not
-  // serve (msm.hip msm_batch; kzgx_set_latency_table)
-  FixedTable fixed_lat{KZGX_LAT_TABLE_BITS, KZGX_LAT_TABLE_POINTS};
+  // the default table: odd multiples at a bounded window over the first SRS
+  // points, built with the SRS, read by the MSMs the main table does not
+  // serve (msm.hip msm_batch; kzgx_set_default_table); c_req -1 = the
+  // window is picked from the memory budget at each build
+  FixedTable fixed_def{KZGX_DEFAULT_TABLE_BITS, KZGX_DEFAULT_TABLE_POINTS};
   // the workspace bound to stream st (claimed on first use; every lookup
   // refreshes its use stamp).  With more than KZGX_MAX_STREAMS distinct
   // streams the least recently USED slot is rebound once the work of its
@@ -226,8 +243,9 @@ int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap);
 bool window_bits_supported(int c);
 bool fixed_bits_supported(int c);
 int fixed_windows(int curve, int c);
-int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);  // the main and the latency table
+int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);  // the main and the default table
 int fixed_build_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t n_srs);
+int fixed_rebuild_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs);
 void fixed_free(Ctx* ctx);  // the main table
 void fixed_free_table(FixedTable& ft);
 bool fixed_usable(const Ctx* ctx, size_t n);

@@ -579,7 +579,7 @@ __global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* 
     return;
   }
   Affine<C> a;
-  const bool fin = xyzz_to_affine<C>(U, a);
+  const bool fin = xyzz_to_affine_lane<C>(U, a);  // thread 0 alone: scalar-ALU inversion
   affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
   out_inf[b] = fin ? 0u : 1u;
 }
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
   }
   if (t == 0) {
     Affine<C> a;
-    bool fin = xyzz_to_affine<C>(acc, a);
+    bool fin = xyzz_to_affine_lane<C>(acc, a);
     affine_to_canonical<C>(out, a, fin);
     *out_inf = fin ? 0u : 1u;
   }
@@ -861,11 +861,16 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
               uint32_t* d_out_inf, hipStream_t st) {
   const bool bn = ctx->curve == KZGX_CURVE_BN254;
   if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
-  // single calls and small batches inside the latency table's prefix: the
-  // table's two-launch latency path (k_fixed_accum_lat) instead of eight
-  // Pippenger launches whose bucket reduction is a ~20-addition chain
-  if (batch <= ctx->small_batch && fixed_table_usable(ctx->fixed_lat, n))
-    return fixed_msm_table(ctx, ctx->fixed_lat, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
+  // inside the default table's prefix: single calls and small batches take
+  // its one-launch latency path (k_fixed_accum_lat) instead of eight
+  // Pippenger launches whose bucket reduction is a ~20-addition chain;
+  // larger batches its batched kernel when its window beats Pippenger
+  {
+    const FixedTable& d = ctx->fixed_def;
+    const int min_c = ctx->curve == KZGX_CURVE_BN254 ? KZGX_DEFAULT_TABLE_BATCH_MIN_C_BN : KZGX_DEFAULT_TABLE_BATCH_MIN_C_BLS;
+    if (fixed_table_usable(d, n) && (batch <= ctx->small_batch || d.c >= min_c))
+      return fixed_msm_table(ctx, ctx->fixed_def, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
+  }
 // Single MSMs chunk from 2^17 points: below, one un-chunked Pippenger (the
 // segment length shrinks to spread it) has one reduction level less; above,
 // its one-workgroup scan over n / 512 count blocks serialises (measured,

@@ -173,9 +173,120 @@ KZGX_DEV Xyzz<C> xyzz_shfl_xor_add(const Xyzz<C>& acc, int off) {
   return xyzz_add_impl<C>(acc, o);
 }
 
+// ---- the last four fold levels as cooperative additions ------------------
+// A lone wave pays for every instruction it issues whatever the number of
+// lanes doing useful work, so the last levels of a shuffle tree (8, 4, 2, 1
+// additions) leave most lanes idle while one addition's ~14 dependent
+// products run in sequence.  Here a group of 8 lanes computes one addition:
+// its independent products side by side, in 4 rounds --
+//   (U1, U2, S1, S2, ZZ1 ZZ2, ZZZ1 ZZZ2), (P^2, R^2), (P PP, U1 PP, ZZ12 PP),
+//   (ZZZ12 PPP, R (Q - X3), S1 PPP)
+// -- with the operands moved between lanes by ds_bpermute (__shfl).  Same
+// formulas and value bounds as xyzz_add_impl (add-2008-s; Y3 as a difference
+// of two products, < 4m), so the sum is the same group element.  Infinity
+// on either side or equal x (P^2 = 0) in any active group sends the whole
+// level to xyzz_add_impl with the full operands (exact special cases).
+template <class C>
+KZGX_DEV F29<typename C::Fp29> xyzz_field(const Xyzz<C>& p, uint32_t f) {
+  F29<typename C::Fp29> r;
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++)
+    r.v[k] = f == 0 ? p.X.v[k] : f == 1 ? p.Y.v[k] : f == 2 ? p.ZZ.v[k] : p.ZZZ.v[k];
+  return r;
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_shfl(const F29<F>& v, uint32_t src) {
+  F29<F> r;
+#pragma unroll
+  for (int k = 0; k < F::L; k++) r.v[k] = __shfl(v.v[k], (int)src, 64);
+  return r;
+}
+
+template <class F>
+KZGX_DEV F29<F> f29_sel(bool c, const F29<F>& a, const F29<F>& b) {
+  F29<F> r;
+#pragma unroll
+  for (int k = 0; k < F::L; k++) r.v[k] = c ? a.v[k] : b.v[k];
+  return r;
+}
+
+// values V[j], j < 2 half (half <= 8), as held on entry:
+//   bfly: the xor-butterfly state after the off = 32 and 16 shuffle levels
+//         (V[j] in lanes j, j + 16, j + 32, j + 48; lane k offers field k >> 4)
+//   else: a previous level's result (V[j] in group j; lane 8 j + s offers
+//         field s & 3)
+// returns V[g] + V[g + half] in every lane of group g = lane / 8 < half
+// (garbage in the other groups).  Every lane of the wave must call it.
+template <class C>
+KZGX_PT Xyzz<C> xyzz_coop_level(const Xyzz<C>& mine, uint32_t lane, uint32_t half, bool bfly) {
+  using F = typename C::Fp29;
+  const uint32_t g = lane >> 3, s = lane & 7, g8 = lane & ~7u;
+  const bool act = g < half;
+  const uint32_t a = act ? g : 0, b = act ? g + half : half;
+  const F29<F> prov = xyzz_field<C>(mine, bfly ? (lane >> 4) : (lane & 3));
+  auto src = [&](uint32_t j, uint32_t f) -> uint32_t { return bfly ? j + 16 * f : 8 * j + f; };
+  auto full = [&](uint32_t j) -> Xyzz<C> {
+    Xyzz<C> r;
+    r.X = f29_shfl<F>(prov, src(j, 0));
+    r.Y = f29_shfl<F>(prov, src(j, 1));
+    r.ZZ = f29_shfl<F>(prov, src(j, 2));
+    r.ZZZ = f29_shfl<F>(prov, src(j, 3));
+    return r;
+  };
+  const int inf_self = xyzz_is_inf<C>(mine) ? 1 : 0;
+  const int inf_ab = __shfl(inf_self, (int)src(a, 0), 64) | __shfl(inf_self, (int)src(b, 0), 64);
+  if (__any(act && inf_ab)) return xyzz_add<C>(full(a), full(b));
+  // round 1: s = 0..5 -> U1 = X_a ZZ_b, U2 = X_b ZZ_a, S1 = Y_a ZZZ_b,
+  // S2 = Y_b ZZZ_a, ZZ_a ZZ_b, ZZZ_a ZZZ_b (s = 6, 7 repeat s = 0)
+  const bool sb = s == 1 || s == 3;
+  const uint32_t xf = s == 2 || s == 3 ? 1u : s == 4 ? 2u : s == 5 ? 3u : 0u;
+  const uint32_t yf = s == 2 || s == 3 || s == 5 ? 3u : 2u;
+  const F29<F> p1 = f29_mul<F>(f29_shfl<F>(prov, src(sb ? b : a, xf)), f29_shfl<F>(prov, src(sb ? a : b, yf)));
+  // round 2: even lanes P = U2 - U1, PP = P^2; odd lanes R = S2 - S1, RR = R^2
+  const uint32_t k2 = (s & 1) * 2;
+  const F29<F> D = f29_sub<F>(f29_shfl<F>(p1, g8 + k2 + 1), f29_shfl<F>(p1, g8 + k2), F::P2);  // < 4m
+  const F29<F> p2 = f29_sqr<F>(D);
+  // round 3: s = 0 PPP = P PP, 1 Q = U1 PP, 2 ZZ3 = ZZ1 ZZ2 PP
+  const F29<F> PP = f29_shfl<F>(p2, g8);
+  if (__any(act && f29_is_zero_lt2m<F>(PP))) return xyzz_add<C>(full(a), full(b));  // equal x
+  const F29<F> t3 = f29_shfl<F>(p1, g8 + (s == 2 ? 4u : 0u));
+  const F29<F> p3 = f29_mul<F>(f29_sel<F>(s == 0, D, t3), PP);
+  // round 4: s = 0 ZZZ3 = ZZZ1 ZZZ2 PPP, 1 R (Q - X3), 2 S1 PPP
+  const F29<F> RR = f29_shfl<F>(p2, g8 + 1);
+  const F29<F> PPP = f29_shfl<F>(p3, g8);
+  const F29<F> Qv = f29_shfl<F>(p3, g8 + 1);
+  Xyzz<C> r;
+  r.X = f29_sub<F>(RR, f29_add<F>(PPP, f29_add<F>(Qv, Qv)), F::P6);  // < 8m
+  const F29<F> t4 = f29_shfl<F>(p1, g8 + (s == 0 ? 5u : 2u));
+  const F29<F> p4 = f29_mul<F>(f29_sel<F>(s == 1, D, t4), f29_sel<F>(s == 1, f29_sub<F>(Qv, r.X, F::P8), PPP));
+  r.ZZ = f29_shfl<F>(p3, g8 + 2);
+  r.ZZZ = f29_shfl<F>(p4, g8);
+  r.Y = f29_sub<F>(f29_shfl<F>(p4, g8 + 1), f29_shfl<F>(p4, g8 + 2), F::P2);  // R (Q - X3) - S1 PPP, < 4m
+  return r;
+}
+
+// a full 64-lane xor-butterfly sum (every lane holds a partial): two
+// shuffle levels, then the four cooperative ones; the sum lands in lanes 0-7
+// (coop = false: six shuffle levels, the sum in every lane)
+template <class C>
+KZGX_PT Xyzz<C> xyzz_wave_sum(Xyzz<C> acc, uint32_t lane, bool coop) {
+  if (!coop) {
+#pragma unroll 1
+    for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
+    return acc;
+  }
+  acc = xyzz_shfl_xor_add<C>(acc, 32);
+  acc = xyzz_shfl_xor_add<C>(acc, 16);
+  acc = xyzz_coop_level<C>(acc, lane, 8, true);
+#pragma unroll 1
+  for (uint32_t h = 4; h >= 1; h >>= 1) acc = xyzz_coop_level<C>(acc, lane, h, false);
+  return acc;
+}
+
 template <class C>
 KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
-                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf);
+                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf, bool coop);
 
 // thread (g, i): point i < n_pad of MSM b, windows [g WG, min(W, (g + 1) WG));
 // wavefront partial q = (g n_pad + i) / 64 -> part[b][q]
@@ -185,7 +296,8 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
                                                         const uint32_t* __restrict__ tab, TabStrides ts,
                                                         const uint8_t* __restrict__ inf, int WG, uint32_t Q,
                                                         uint32_t* __restrict__ part, uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+                                                        uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                        int coop) {
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
@@ -218,8 +330,7 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
       acc = xyzz_add_affine_impl<C>(acc, cur);
     }
   }
-#pragma unroll 1
-  for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
+  acc = xyzz_wave_sum<C>(acc, threadIdx.x, coop != 0);  // lane 0 holds the wavefront's sum
   // the last of MSM b's Q wavefronts to finish folds the Q partials (one
   // launch per call instead of two): release the partial, count it in
   // (device-scope atomic), and the wavefront that counts the Q-th acquires
@@ -233,7 +344,7 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
   prev = __shfl(prev, 0, 64);
   if (prev + 1 != Q) return;
   __threadfence();
-  lat_fold_finish<C>(part, Q, b, threadIdx.x, out, out_inf);
+  lat_fold_finish<C>(part, Q, b, threadIdx.x, out, out_inf, coop != 0);
   if (threadIdx.x == 0) cnt[b] = 0;  // ready for the next call (stream order)
 }
 
@@ -241,19 +352,29 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
 // Q, a shuffle tree over the lanes that hold any, lane 0 converts and stores
 template <class C>
 KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
-                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf, bool coop) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t* p = part + (size_t)b * Q * XW;
   Xyzz<C> acc = lane < Q ? xyzz_load<C>(p + (size_t)lane * XW) : xyzz_inf<C>();
 #pragma unroll 1
   for (uint32_t k = lane + 64; k < Q; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(p + (size_t)k * XW));
+  if (coop && Q > 16) {  // the full butterfly (lanes >= Q hold the identity)
+    acc = xyzz_wave_sum<C>(acc, lane, true);
+    if (lane == 0) {
+      Affine<C> a;
+      const bool fin = xyzz_to_affine_lane<C>(acc, a);
+      affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+      out_inf[b] = fin ? 0u : 1u;
+    }
+    return;
+  }
   int off = 32;
   while (off > 1 && (uint32_t)off >= Q) off >>= 1;  // lanes >= Q hold the identity
 #pragma unroll 1
   for (; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
-  if (lane == 0) {
+  if (lane == 0) {  // lane 0 alone: its inversion on the scalar ALU
     Affine<C> a;
-    const bool fin = xyzz_to_affine<C>(acc, a);
+    const bool fin = xyzz_to_affine_lane<C>(acc, a);
     affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
     out_inf[b] = fin ? 0u : 1u;
   }
@@ -470,9 +591,38 @@ int fixed_build_table(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t 
                                         : fixed_build_impl<BLS12381G1>(ctx, ft, d_canon, n);
 }
 
+// the default table: a fixed window, or (c_req < 0) the widest c <= 12 whose
+// table fits KZGX_DEFAULT_TABLE_PERMILLE of the device memory and the free
+// memory less 4 GiB; none if even c = 7 does not
+static int fixed_build_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
+  FixedTable& ft = ctx->fixed_def;
+  if (ft.c_req >= 0) return fixed_build_table(ctx, ft, d_canon, n_srs);
+  if (ft.n_req == 0) return KZGX_OK;
+  fixed_free_table(ft);  // its memory counts as free for the choice
+  const size_t n = ft.n_req < n_srs ? ft.n_req : n_srs;
+  size_t free_b = 0, total_b = 0;
+  KZGX_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
+  const size_t margin = (size_t)4 << 30;
+  size_t budget = total_b / 1000 * KZGX_DEFAULT_TABLE_PERMILLE;
+  if (free_b < margin) return KZGX_OK;
+  if (budget > free_b - margin) budget = free_b - margin;
+  for (int c = 12; c >= 7; c--) {
+    if (fixed_table_bytes(ctx->curve, c, n) > budget) continue;
+    ft.c_req = c;
+    const int rc = fixed_build_table(ctx, ft, d_canon, n_srs);
+    ft.c_req = -1;  // the next SRS picks again
+    return rc == KZGX_ERR_OOM ? KZGX_OK : rc;  // no room after all: no default table
+  }
+  return KZGX_OK;
+}
+
 int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
   KZGX_TRY(fixed_build_table(ctx, ctx->fixed, d_canon, n_srs));
-  return fixed_build_table(ctx, ctx->fixed_lat, d_canon, n_srs);
+  return fixed_build_default(ctx, d_canon, n_srs);
+}
+
+int fixed_rebuild_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
+  return fixed_build_default(ctx, d_canon, n_srs);
 }
 
 void fixed_free(Ctx* ctx) { fixed_free_table(ctx->fixed); }
@@ -512,10 +662,12 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
       KZGX_TRY_HIP(hipMalloc((void**)&wsp->lat_cnt, 64 * sizeof(uint32_t)));
       KZGX_TRY_HIP(hipMemsetAsync(wsp->lat_cnt, 0, 64 * sizeof(uint32_t), st));
     }
+    // KZGX_NO_LAT_COOP: the last fold levels as plain shuffle additions (A/B)
+    static const bool coop_off = std::getenv("KZGX_NO_LAT_COOP") != nullptr;
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
                        (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), WG, Q, wsp->fpart,
-                       wsp->lat_cnt, d_out, d_out_inf);
+                       wsp->lat_cnt, d_out, d_out_inf, coop_off ? 0 : 1);
     KZGX_TRY_HIP(hipGetLastError());
     return KZGX_OK;
   }
@@ -846,7 +998,8 @@ int microbench_mixed_add(Ctx* ctx, double* rate) {
 // constant-rate wall clock and its core-clock counter inside the kernel
 // (no launch overhead).  op: 0 Montgomery product, 1 Fermat inversion,
 // 2 binary-Euclid inversion, 3 XYZZ addition, 4 mixed addition, 5 XYZZ ->
-// affine conversion.
+// affine conversion, 6 / 7 the same as 2 / 5 on the scalar ALU (one lane's
+// value made wave-uniform).
 // --------------------------------------------------------------------------
 template <class C>
 __global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict__ pts, int op, uint32_t iters,
@@ -866,7 +1019,12 @@ __global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict
     else if (op == 2) a = f29_inv_vt<F, C::Fp::N>(a, C::Fp::P);
     else if (op == 3) acc = xyzz_add_impl<C>(acc, qx);
     else if (op == 4) acc = xyzz_add_affine_impl<C>(acc, q);
-    else {
+    else if (op == 6) a = f29_inv_uniform<F, C::Fp::N>(a, C::Fp::P);
+    else if (op == 7) {
+      Affine<C> r;
+      (void)xyzz_to_affine_impl<C, true>(acc, r);
+      acc.X = r.y;
+    } else {
       Affine<C> r;
       (void)xyzz_to_affine_impl<C>(acc, r);
       acc.X = r.y;  // next input depends on this output
@@ -910,7 +1068,7 @@ static int debug_latency_impl(Ctx* ctx, int op, uint32_t iters, double* res) {
 }
 
 int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res) {
-  if (op < 0 || op > 5 || iters == 0) return KZGX_ERR_ARG;
+  if (op < 0 || op > 7 || iters == 0) return KZGX_ERR_ARG;
   return ctx->curve == KZGX_CURVE_BN254 ? debug_latency_impl<BN254G1>(ctx, op, iters, res)
                                         : debug_latency_impl<BLS12381G1>(ctx, op, iters, res);
 }

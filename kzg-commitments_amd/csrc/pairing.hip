@@ -393,7 +393,7 @@ __global__ void k_g1_sub(const uint32_t* __restrict__ a, const uint32_t* __restr
   if (affine_from_canonical<C>(a, pa) && !(a_inf && *a_inf)) acc = xyzz_from_affine<C>(pa);
   if (affine_from_canonical<C>(b, pb) && !(b_inf && *b_inf)) acc = xyzz_add_affine<C>(acc, affine_neg<C>(pb));
   Affine<C> r;
-  const bool fin = xyzz_to_affine<C>(acc, r);
+  const bool fin = xyzz_to_affine_lane<C>(acc, r);  // thread 0 alone
   affine_to_canonical<C>(out, r, fin);
   *out_inf = fin ? 0u : 1u;
 }

@@ -83,9 +83,29 @@ def kernel_symbols(elf: bytes):
     return out
 
 
+def mask_pc_relative(code: bytes) -> bytes:
+    """the code with the PC-relative offsets of its calls and constant
+    addresses zeroed: `s_getpc_b64 s[n:n+1]` (SOP1, op 0x1c) followed by
+    `s_add_u32` / `s_addc_u32` with a 32-bit literal (SOP2, src1 = 0xff).
+    Those literals move whenever any other function of the code object moves
+    (a kernel's calls to its out-of-line rare paths), so without this a change
+    elsewhere in the translation unit would change the kernel's identity."""
+    b = bytearray(code)
+    for i in range(0, len(b) - 20, 4):
+        w, = struct.unpack_from("<I", b, i)
+        if (w & 0xFF80FF00) != 0xBE801C00:
+            continue
+        for k in (4, 12):
+            w2, = struct.unpack_from("<I", b, i + k)
+            if (w2 >> 30) == 2 and ((w2 >> 8) & 0xFF) == 0xFF:
+                b[i + k + 4:i + k + 8] = b"\0\0\0\0"
+    return bytes(b)
+
+
 def kernel_hash(so_path: str, *name_parts: str, target: str = "gfx950") -> dict:
     """SHA-256 over the machine code of every function whose mangled name
-    contains all of name_parts (sorted by name), with the symbols hashed"""
+    contains all of name_parts (sorted by name), with the symbols hashed and
+    PC-relative offsets masked (mask_pc_relative)"""
     h = hashlib.sha256()
     found = []
     for img in device_images(so_path, target):
@@ -95,9 +115,9 @@ def kernel_hash(so_path: str, *name_parts: str, target: str = "gfx950") -> dict:
     found.sort()
     for name, code in found:
         h.update(name.encode() + b"\0")
-        h.update(code)
+        h.update(mask_pc_relative(code))
     return {"sha256": h.hexdigest() if found else None, "symbols": [n for n, _ in found],
-            "bytes": sum(len(c) for _, c in found)}
+            "bytes": sum(len(c) for _, c in found), "hash": "sha256 of name + code, PC-relative offsets masked"}
 
 
 def fixed_accum_parts(curve: str, c: int):

@@ -23,7 +23,7 @@ EXPORTS = [
     "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
-    "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout", "kzgx_set_latency_table", "kzgx_latency_table_info",
+    "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout", "kzgx_set_default_table", "kzgx_default_table_info",
     "kzgx_microbench_mad_u64", "kzgx_microbench_mad_u64_clock", "kzgx_clock_probe", "kzgx_set_fixed_points_per_thread", "kzgx_set_small_batch", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
@@ -81,8 +81,8 @@ def lib():
             "kzgx_fixed_base_bytes": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, sz, ctypes.POINTER(sz)]),
             "kzgx_set_fixed_base_budget": (ctypes.c_int, [vp, sz, sz, intp]),
             "kzgx_set_fixed_base_layout": (ctypes.c_int, [vp, ctypes.c_int]),
-            "kzgx_set_latency_table": (ctypes.c_int, [vp, ctypes.c_int, sz]),
-            "kzgx_latency_table_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+            "kzgx_set_default_table": (ctypes.c_int, [vp, ctypes.c_int, sz]),
+            "kzgx_default_table_info": (ctypes.c_int, [vp, intp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
             "kzgx_fixed_base_layout": (ctypes.c_int, [vp, intp]),
             "kzgx_microbench_mad_u64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
             "kzgx_microbench_mad_u64_clock": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
@@ -173,14 +173,14 @@ class Context:
         _chk(lib().kzgx_create(ctypes.byref(h), CURVES[curve], device), "kzgx_create")
         self.h = h
 
-    def set_latency_table(self, c: int, n_points: int = 4097):
-        """kzgx_set_latency_table: c = 0 turns the single-call table off"""
-        _chk(lib().kzgx_set_latency_table(self.h, c, n_points if c else 0), "kzgx_set_latency_table")
+    def set_default_table(self, c: int, n_points: int = 4097):
+        """kzgx_set_default_table: c = -1 the budget-chosen window, 0 off"""
+        _chk(lib().kzgx_set_default_table(self.h, c, n_points if c else 0), "kzgx_set_default_table")
 
-    def latency_table_info(self):
+    def default_table_info(self):
         c, n, b = ctypes.c_int(0), ctypes.c_size_t(0), ctypes.c_size_t(0)
-        _chk(lib().kzgx_latency_table_info(self.h, ctypes.byref(c), ctypes.byref(n), ctypes.byref(b)),
-             "kzgx_latency_table_info")
+        _chk(lib().kzgx_default_table_info(self.h, ctypes.byref(c), ctypes.byref(n), ctypes.byref(b)),
+             "kzgx_default_table_info")
         return c.value, n.value, b.value
 
     def debug_ws_read(self, name: str, nbytes: int) -> np.ndarray:

@@ -35,9 +35,9 @@ def ctx_factory():
         if curve not in made:
             made[curve] = kzgx.Context(curve)
             # the parity tests built on this factory target the table-less
-            # Pippenger path: single calls would otherwise take the default
-            # latency table (tests/test_gpu_latency_table.py covers that)
-            made[curve].set_latency_table(0)
+            # Pippenger path: MSMs would otherwise take the default table
+            # (tests/test_gpu_default_table.py covers that)
+            made[curve].set_default_table(0)
         return made[curve]
 
     yield get

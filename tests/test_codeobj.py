@@ -36,3 +36,19 @@ def test_traffic_needs_the_same_kernel(tmp_path, monkeypatch):
     assert bench.matching_traffic("cfg2", 2048, 17, "cd" * 32) == (None, None)
     assert bench.matching_traffic("cfg2", 1024, 17, "ab" * 32) == (None, None)
     assert bench.matching_traffic("cfg2", 2048, 17, None) == (None, None)
+
+
+def test_pc_relative_offsets_do_not_change_the_identity():
+    """a call's s_getpc_b64 + s_add_u32 / s_addc_u32 literals move when other
+    code moves; they are masked, every other word is kept"""
+    import struct
+    import codeobj
+
+    def code(lit_lo, lit_hi, tail):
+        words = [0xBF800000, 0xBE901C00, 0x8010FF10, lit_lo, 0x8211FF11, lit_hi, tail, 0xBF800000, 0xBF800000]
+        return struct.pack("<%dI" % len(words), *words)
+
+    a = codeobj.mask_pc_relative(code(0xFFFFEC9C, 0xFFFFFFFF, 0x7E000280))
+    b = codeobj.mask_pc_relative(code(0x00001234, 0x00000000, 0x7E000280))
+    c = codeobj.mask_pc_relative(code(0x00001234, 0x00000000, 0x7E000281))
+    assert a == b and a != c

@@ -1,8 +1,10 @@
-"""The default latency table (kzgx_set_latency_table, Ctx::fixed_lat): odd
-multiples at c = 8 over the first 4097 SRS points, built with the SRS, read
-by batches of <= 16 MSMs that fit in it -- every single create_commit /
-create_proof of degree <= 4096 (the reference's benchmark calls,
-benchmark/benchmark.cpp:40-66).  Checked against the known-tau identity
+"""The default table (kzgx_set_default_table, Ctx::fixed_def): odd multiples
+over the first 4097 SRS points at the widest window c <= 12 that fits 2.5% of
+the HBM (BN254 c = 11, BLS12-381 c = 10 on an MI355X), built with the SRS,
+read by the MSMs that fit in it -- every single create_commit / create_proof
+of degree <= 4096 (the reference's benchmark calls,
+benchmark/benchmark.cpp:40-66) through the one-launch path, larger batches
+through the batched kernel.  Checked against the known-tau identity
 commit = [P(tau)]G1 / proof = [q(tau)]G1 (oracle), at the sizes around the
 table's edges, on both curves, with a degenerate SRS, and with the table off
 or too short (Pippenger)."""
@@ -44,12 +46,17 @@ def lat_ctx():
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-def test_latency_table_is_built_by_default(name, C, lat_ctx):
+def test_default_table_is_built_by_default(name, C, lat_ctx):
     import kzgx
+    import torch
     ctx = lat_ctx(name, C)
-    c, n, b = ctx.latency_table_info()
-    assert (c, n) == (8, 4097)
-    assert b == kzgx.fixed_base_bytes(name, 8, 4097)
+    c, n, b = ctx.default_table_info()
+    total = torch.cuda.get_device_properties(0).total_memory
+    budget = total // 1000 * 25
+    assert n == 4097 and 7 <= c <= 12
+    assert b == kzgx.fixed_base_bytes(name, c, 4097) <= budget
+    if c < 12:  # the widest that fits (the free-memory cap aside)
+        assert kzgx.fixed_base_bytes(name, c + 1, 4097) > budget or torch.cuda.mem_get_info()[0] < (8 << 30)
     assert ctx.fixed_base_info()[0] == 0  # the main (throughput) table stays opt-in
 
 
@@ -67,9 +74,10 @@ def test_single_commit_matches_oracle(name, C, n, lat_ctx):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-@pytest.mark.parametrize("batch", [2, 16, 17])
+@pytest.mark.parametrize("batch", [2, 16, 17, 64])
 def test_small_batches(name, C, batch, lat_ctx):
-    """<= 16 MSMs take the table, 17 the batched Pippenger"""
+    """<= 16 MSMs take the one-launch path, more the batched table kernel
+    (c >= 10) or the batched Pippenger"""
     ctx = lat_ctx(name, C)
     tau = K.default_tau(C)
     n = 300
@@ -94,24 +102,30 @@ def test_single_proofs(name, C, lat_ctx):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-def test_latency_table_off_and_degenerate(name, C):
+def test_default_table_off_and_degenerate(name, C):
     """c = 0 turns it off (Pippenger); tau = 0 (every SRS point but the
     first infinite) still exact through the table"""
     import kzgx
     ctx = kzgx.Context(name)
     try:
         ctx.gen_srs(0, 200)
-        assert ctx.latency_table_info()[:2] == (8, 200)
+        c0, n0, _ = ctx.default_table_info()
+        assert n0 == 200 and c0 >= 7
         P = K.random_scalars(C, 150, seed=7700)
         out, inf = ctx.msm(limbs(P))
         assert pt(name, out, inf) == K.commit_via_tau(C, 0, P)
-        ctx.set_latency_table(0)
-        assert ctx.latency_table_info() == (0, 0, 0)
+        ctx.set_default_table(0)
+        assert ctx.default_table_info() == (0, 0, 0)
         out2, inf2 = ctx.msm(limbs(P))
         assert pt(name, out2, inf2) == K.commit_via_tau(C, 0, P)
-        ctx.set_latency_table(7, 100)  # rebuilt at once over the installed SRS
-        assert ctx.latency_table_info()[:2] == (7, 100)
+        ctx.set_default_table(7, 100)  # rebuilt at once over the installed SRS
+        assert ctx.default_table_info()[:2] == (7, 100)
         out3, inf3 = ctx.msm(limbs(P[:90]))
         assert pt(name, out3, inf3) == K.commit_via_tau(C, 0, P[:90])
+        ctx.set_default_table(-1)  # back to the budget's choice (4097 points, clamped to the SRS)
+        assert ctx.default_table_info()[:2] == (c0, 200)
+        outb, infb = ctx.msm_batch(np.concatenate([limbs(P[:90])] * 20), 90, 20)
+        for b in range(20):
+            assert pt(name, outb[b], infb[b]) == K.commit_via_tau(C, 0, P[:90]), b
     finally:
         ctx.close()
