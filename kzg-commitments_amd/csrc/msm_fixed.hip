@@ -159,18 +159,32 @@ __global__ __launch_bounds__(64) void k_fixed_finish(const uint32_t* __restrict_
 //     Q <= 256 wavefront partials, which then converts to affine in lane 0)
 // instead of W mixed additions + two 64:1 fold levels + a separate finish.
 // --------------------------------------------------------------------------
+// lane l and lane l ^ off both add the pair, the lower lane's value first:
+// the same operands in the same order give bit-identical XYZZ values in both
+// lanes (the addition is not symmetric in representation: swapping the
+// operands negates P, hence Y3 and ZZZ3), which xyzz_coop_level's butterfly
+// layout relies on when it reads one point's fields from different lanes
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_shfl_xor_add(const Xyzz<C>& acc, int off) {
   constexpr int L = C::Fp29::L;
-  Xyzz<C> o;
+  const bool hi = (threadIdx.x & (unsigned)off) != 0;
+  Xyzz<C> o, a, b;
 #pragma unroll
   for (int k = 0; k < L; k++) {
     o.X.v[k] = __shfl_xor(acc.X.v[k], off, 64);
     o.Y.v[k] = __shfl_xor(acc.Y.v[k], off, 64);
     o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], off, 64);
     o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], off, 64);
+    a.X.v[k] = hi ? o.X.v[k] : acc.X.v[k];
+    a.Y.v[k] = hi ? o.Y.v[k] : acc.Y.v[k];
+    a.ZZ.v[k] = hi ? o.ZZ.v[k] : acc.ZZ.v[k];
+    a.ZZZ.v[k] = hi ? o.ZZZ.v[k] : acc.ZZZ.v[k];
+    b.X.v[k] = hi ? acc.X.v[k] : o.X.v[k];
+    b.Y.v[k] = hi ? acc.Y.v[k] : o.Y.v[k];
+    b.ZZ.v[k] = hi ? acc.ZZ.v[k] : o.ZZ.v[k];
+    b.ZZZ.v[k] = hi ? acc.ZZZ.v[k] : o.ZZZ.v[k];
   }
-  return xyzz_add_impl<C>(acc, o);
+  return xyzz_add_impl<C>(a, b);
 }
 
 // ---- the last four fold levels as cooperative additions ------------------
@@ -285,11 +299,18 @@ KZGX_PT Xyzz<C> xyzz_wave_sum(Xyzz<C> acc, uint32_t lane, bool coop) {
 }
 
 template <class C>
-KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
-                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf, bool coop);
+KZGX_DEV Xyzz<C> lat_fold(const uint32_t* __restrict__ p, uint32_t Q, uint32_t lane, bool coop);
+template <class C>
+KZGX_DEV void lat_store_affine(const Xyzz<C>& acc, uint32_t b, uint32_t lane, uint32_t* __restrict__ out,
+                               uint32_t* __restrict__ out_inf);
 
 // thread (g, i): point i < n_pad of MSM b, windows [g WG, min(W, (g + 1) WG));
-// wavefront partial q = (g n_pad + i) / 64 -> part[b][q]
+// wavefront partial q = (g n_pad + i) / 64 -> part[b][q].  NG = 1: the last
+// of the Q wavefronts folds all Q partials; NG > 1 (Q > 128): the last
+// wavefront of each group of 64 folds its group into part2[b][group], and the
+// last of the NG group folders folds those (two fold levels of <= 64
+// partials each instead of one wavefront summing Q / 64 partials per lane).
+// cnt[b (NG + 1)]: the final arrival counter, then one per group.
 template <class C, int CB>
 __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restrict__ scalars, uint32_t n,
                                                         uint32_t n_pad, size_t stride_words,
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
                                                         const uint8_t* __restrict__ inf, int WG, uint32_t Q,
                                                         uint32_t* __restrict__ part, uint32_t* __restrict__ cnt,
                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
-                                                        int coop) {
+                                                        int coop, uint32_t NG, uint32_t* __restrict__ part2) {
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
@@ -335,44 +356,61 @@ __global__ __launch_bounds__(64) void k_fixed_accum_lat(const uint32_t* __restri
   // launch per call instead of two): release the partial, count it in
   // (device-scope atomic), and the wavefront that counts the Q-th acquires
   // the others and runs the fold
+  const uint32_t q = t / 64, lane = threadIdx.x;
+  uint32_t* cb = cnt + (size_t)b * (NG + 1);
+  const uint32_t grp = q >> 6;
   uint32_t prev = 0;
-  if (threadIdx.x == 0) {
-    xyzz_store<C>(part + ((size_t)b * Q + t / 64) * XW, acc);
+  if (lane == 0) {
+    xyzz_store<C>(part + ((size_t)b * Q + q) * XW, acc);
     __threadfence();
-    prev = atomicAdd(cnt + b, 1u);
+    prev = atomicAdd(NG > 1 ? cb + 1 + grp : cb, 1u);
   }
   prev = __shfl(prev, 0, 64);
-  if (prev + 1 != Q) return;
-  __threadfence();
-  lat_fold_finish<C>(part, Q, b, threadIdx.x, out, out_inf, coop != 0);
-  if (threadIdx.x == 0) cnt[b] = 0;  // ready for the next call (stream order)
+  if (NG > 1) {
+    const uint32_t gsz = Q - grp * 64 < 64 ? Q - grp * 64 : 64;
+    if (prev + 1 != gsz) return;
+    __threadfence();
+    const Xyzz<C> gs = lat_fold<C>(part + ((size_t)b * Q + grp * 64) * XW, gsz, lane, coop != 0);
+    if (lane == 0) {
+      cb[1 + grp] = 0;  // every arrival of the group is in
+      xyzz_store<C>(part2 + ((size_t)b * NG + grp) * XW, gs);
+      __threadfence();
+      prev = atomicAdd(cb, 1u);
+    }
+    prev = __shfl(prev, 0, 64);
+    if (prev + 1 != NG) return;
+    __threadfence();
+    lat_store_affine<C>(lat_fold<C>(part2 + (size_t)b * NG * XW, NG, lane, coop != 0), b, lane, out, out_inf);
+  } else {
+    if (prev + 1 != Q) return;
+    __threadfence();
+    lat_store_affine<C>(lat_fold<C>(part + (size_t)b * Q * XW, Q, lane, coop != 0), b, lane, out, out_inf);
+  }
+  if (lane == 0) cb[0] = 0;  // ready for the next call (stream order)
 }
 
-// MSM b's fold by one wavefront: lane sums partials lane, lane + 64, ... <
-// Q, a shuffle tree over the lanes that hold any, lane 0 converts and stores
+// the sum of Q partials p[0..Q) by one wavefront, in lane 0: lane sums
+// partials lane, lane + 64, ... < Q, then a butterfly (cooperative last
+// levels) or a shuffle tree over the lanes that hold any
 template <class C>
-KZGX_DEV void lat_fold_finish(const uint32_t* __restrict__ part, uint32_t Q, uint32_t b, uint32_t lane,
-                              uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf, bool coop) {
+KZGX_DEV Xyzz<C> lat_fold(const uint32_t* __restrict__ p, uint32_t Q, uint32_t lane, bool coop) {
   constexpr int XW = xyzz_words<C>();
-  const uint32_t* p = part + (size_t)b * Q * XW;
   Xyzz<C> acc = lane < Q ? xyzz_load<C>(p + (size_t)lane * XW) : xyzz_inf<C>();
 #pragma unroll 1
   for (uint32_t k = lane + 64; k < Q; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(p + (size_t)k * XW));
-  if (coop && Q > 16) {  // the full butterfly (lanes >= Q hold the identity)
-    acc = xyzz_wave_sum<C>(acc, lane, true);
-    if (lane == 0) {
-      Affine<C> a;
-      const bool fin = xyzz_to_affine_lane<C>(acc, a);
-      affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
-      out_inf[b] = fin ? 0u : 1u;
-    }
-    return;
-  }
+  if (coop && Q > 16) return xyzz_wave_sum<C>(acc, lane, true);  // the full butterfly (lanes >= Q: identity)
   int off = 32;
   while (off > 1 && (uint32_t)off >= Q) off >>= 1;  // lanes >= Q hold the identity
 #pragma unroll 1
   for (; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
-  if (lane == 0) {  // lane 0 alone: its inversion on the scalar ALU
+  return acc;
+}
+
+// lane 0 converts MSM b's sum and stores it (its inversion on the scalar ALU)
+template <class C>
+KZGX_DEV void lat_store_affine(const Xyzz<C>& acc, uint32_t b, uint32_t lane, uint32_t* __restrict__ out,
+                               uint32_t* __restrict__ out_inf) {
+  if (lane == 0) {
     Affine<C> a;
     const bool fin = xyzz_to_affine_lane<C>(acc, a);
     affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
@@ -648,26 +686,33 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
   const size_t n_pad = (n + 63) / 64 * 64;
   if (batch <= 16 && !xyzz_out && n_pad <= 16384 && ft.pts_per_thread == 0 && !lat_off) {
     constexpr int W = FixedWin<C, CB>::W;
-    // G window groups of WG windows: up to 256 wavefront partials per MSM
-    // (degree 4096: 3 groups of 5 windows; one group of 15 made the
-    // accumulation chain 15 additions long)
-    int G = (int)std::min<size_t>(W, std::max<size_t>(1, 16384 / n_pad));
+    // G window groups of WG windows over up to 2^14 threads per MSM
+    // (KZGX_LAT_THREADS: the single-MSM count, A/B; 2^16 measured slower:
+    // degree 4096 0.233 vs 0.202 ms, profiles/r04_lat_ab_coop_threads.txt):
+    // degree 4096 takes 3 groups of 8 windows (195 wavefront partials,
+    // folded in two levels), degree 128 one window per thread
+    static const size_t lat_threads = std::getenv("KZGX_LAT_THREADS") ? std::strtoul(std::getenv("KZGX_LAT_THREADS"), nullptr, 10) : 16384;
+    const size_t per_msm = std::max<size_t>(std::min<size_t>(lat_threads, 16384), lat_threads / batch);
+    int G = (int)std::min<size_t>(W, std::max<size_t>(1, per_msm / n_pad));
     const int WG = (W + G - 1) / G;
     G = (W + WG - 1) / WG;
-    const uint32_t Q = (uint32_t)(n_pad * G / 64);  // <= 256
+    const uint32_t Q = (uint32_t)(n_pad * G / 64);
+    const uint32_t NG = Q > 128 ? (Q + 63) / 64 : 1;  // <= 16
     WsLease wsp = ctx->ws_for(st);
     if (!wsp) return KZGX_ERR_ARG;
-    KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * Q * XB, &wsp->fpart_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&wsp->fpart, batch * (Q + NG) * XB, &wsp->fpart_b));
+    constexpr size_t kCnt = 16 * 17;  // batch <= 16 MSMs x (NG <= 16 groups + 1)
     if (!wsp->lat_cnt) {  // per-MSM arrival counters, zero between calls
-      KZGX_TRY_HIP(hipMalloc((void**)&wsp->lat_cnt, 64 * sizeof(uint32_t)));
-      KZGX_TRY_HIP(hipMemsetAsync(wsp->lat_cnt, 0, 64 * sizeof(uint32_t), st));
+      KZGX_TRY_HIP(hipMalloc((void**)&wsp->lat_cnt, kCnt * sizeof(uint32_t)));
+      KZGX_TRY_HIP(hipMemsetAsync(wsp->lat_cnt, 0, kCnt * sizeof(uint32_t), st));
     }
+    if (NG > 16 || batch * (NG + 1) > kCnt) return KZGX_ERR_ARG;  // unreachable: Q <= 2^16 / 64
     // KZGX_NO_LAT_COOP: the last fold levels as plain shuffle additions (A/B)
     static const bool coop_off = std::getenv("KZGX_NO_LAT_COOP") != nullptr;
     ProfScope p(ctx, st, "msm_accum");
     hipLaunchKernelGGL((k_fixed_accum_lat<C, CB>), dim3(Q, (unsigned)batch), dim3(64), 0, st, d_scalars, (uint32_t)n,
                        (uint32_t)n_pad, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), WG, Q, wsp->fpart,
-                       wsp->lat_cnt, d_out, d_out_inf, coop_off ? 0 : 1);
+                       wsp->lat_cnt, d_out, d_out_inf, coop_off ? 0 : 1, NG, wsp->fpart + batch * Q * XB / 4);
     KZGX_TRY_HIP(hipGetLastError());
     return KZGX_OK;
   }

@@ -39,6 +39,14 @@ KZGX_DEV Fe<FR> fe_shfl_down(const Fe<FR>& a, int d) {
 }
 
 template <class FR>
+KZGX_DEV Fe<FR> fe_shfl(const Fe<FR>& a, uint32_t src) {
+  Fe<FR> r;
+#pragma unroll
+  for (int i = 0; i < FR::N; i++) r.v[i] = __shfl(a.v[i], (int)src, 64);
+  return r;
+}
+
+template <class FR>
 KZGX_DEV Fe<FR> fe_shfl_xor(const Fe<FR>& a, int m) {
   Fe<FR> r;
 #pragma unroll
@@ -115,6 +123,69 @@ __global__ __launch_bounds__(256) void k_quotient_single(const uint32_t* __restr
       fe_store<FR>(ys + (size_t)j * N, h);
   }
   if (n == 0 && lane == 0 && ys) fe_store<FR>(ys + (size_t)j * N, fe_zero<FR>());
+}
+
+// Mid-size single openings (batch <= 4, 2^9 <= n <= 2^14): the three phases
+// in ONE workgroup of NWV wavefronts per opening, so one launch and no global
+// round trips.  Thread t owns [t L, t L + L), L = ceil(n / (64 NWV)):
+//   local Horner; a wavefront suffix scan of (c, pw) with multiplier z^L, pw
+//   = z^(L (63 - lane)) as a suffix product in the same 6 steps; the NWV
+//   wavefront totals H_w through LDS, each wavefront scanning them itself
+//   (log2 NWV steps, multiplier Z = z^(64 L), the scan's last power) into
+//   C_w = h at the top of wavefront w and y = h_0; carry-in c_{t+1} + C_w pw;
+//   replay.  NWV = 4: one wavefront per SIMD of the CU -- a lone wavefront
+//   issues every cycle its SIMD offers, 16 would share each SIMD four ways
+//   and run every product of the chain 4x slower (measured: 1024 threads lost
+//   to the chip-wide kernel).
+template <class FR, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_quotient_wg(const uint32_t* __restrict__ coeffs, uint32_t n,
+                                                          size_t cstride, const uint32_t* __restrict__ zs,
+                                                          uint32_t* __restrict__ q, size_t qstride,
+                                                          uint32_t* __restrict__ ys) {
+  constexpr int N = FR::N;
+  __shared__ uint32_t sh[NWV * N];
+  const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t* P = coeffs + (size_t)j * cstride;
+  const Fe<FR> zm = fe_to_mont<FR>(fe_load<FR>(zs + (size_t)j * N));
+  const uint32_t L = (n + 64 * NWV - 1) / (64 * NWV);
+  const uint32_t lo = min(t * L, n), hi = min(lo + L, n);
+  Fe<FR> h = fe_zero<FR>();
+  for (uint32_t k = hi; k-- > lo;) h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+  const Fe<FR> zL = fe_pow_u32<FR>(zm, L);
+  Fe<FR> c = h, zp = zL, pw = lane < 63 ? zL : fe_one<FR>();
+#pragma unroll
+  for (int s = 0; s < 6; s++) {
+    const Fe<FR> o = fe_shfl_down<FR>(c, 1 << s), po = fe_shfl_down<FR>(pw, 1 << s);
+    if (lane + (1u << s) < 64) {
+      c = fe_add<FR>(c, fe_mul<FR>(o, zp));  // canonical * Montgomery = canonical
+      pw = fe_mul<FR>(pw, po);
+    }
+    zp = fe_sqr<FR>(zp);
+  }
+  // zp = z^(64 L); c at lane 0 = the wavefront's total H_w
+  if (lane == 0) fe_store<FR>(sh + wv * N, c);
+  __syncthreads();
+  Fe<FR> S = lane < NWV ? fe_load<FR>(sh + lane * N) : fe_zero<FR>();
+  Fe<FR> Zp = zp;
+#pragma unroll
+  for (int s = 0; (1 << s) < NWV; s++) {
+    const Fe<FR> o = fe_shfl_down<FR>(S, 1 << s);
+    if (lane + (1u << s) < NWV) S = fe_add<FR>(S, fe_mul<FR>(o, Zp));
+    Zp = fe_sqr<FR>(Zp);
+  }
+  // S at lane v = h at the bottom of wavefront v's span; C_w = S_(w+1)
+  const Fe<FR> Cw = fe_shfl<FR>(S, wv + 1 < NWV ? wv + 1 : NWV);  // lane NWV holds zero
+  const Fe<FR> cn = fe_shfl_down<FR>(c, 1);
+  h = fe_mul<FR>(Cw, pw);
+  if (lane < 63) h = fe_add<FR>(h, cn);
+  uint32_t* Q = q + (size_t)j * qstride;
+  for (uint32_t k = hi; k-- > lo;) {
+    h = fe_add<FR>(fe_load<FR>(P + (size_t)k * N), fe_mul<FR>(h, zm));
+    if (k >= 1)
+      fe_store<FR>(Q + (size_t)(k - 1) * N, h);
+    else if (ys)
+      fe_store<FR>(ys + (size_t)j * N, h);
+  }
 }
 
 // Large single openings (batch <= 4, n >= 2^13): the same three phases spread
@@ -377,6 +448,18 @@ static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, si
     return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)1u << 11;
   }();
   constexpr size_t QBIG_LANES = 1u << 18;  // 4096 wavefronts: 4 per SIMD
+  // one workgroup per opening from QWG_MIN to 2^14 coefficients
+  // (k_quotient_wg; KZGX_QWG_MIN overrides, 0 = never, for A/B)
+  static const size_t QWG_MIN = [] {
+    const char* e = std::getenv("KZGX_QWG_MIN");
+    return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)512;
+  }();
+  if (batch <= 4 && QWG_MIN && n >= QWG_MIN && n <= (1u << 14)) {
+    hipLaunchKernelGGL((k_quotient_wg<FR, 4>), dim3((unsigned)batch), dim3(256), 0, st, d_coeffs, (uint32_t)n, cstride,
+                       d_z, d_q, qstride, d_y);
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
+  }
   if (batch <= 4 && n >= QBIG_N) {
     constexpr int N = FR::N;
     const uint32_t L = (uint32_t)std::max<size_t>(8, (n + QBIG_LANES - 1) / QBIG_LANES);

@@ -89,6 +89,41 @@ def test_small_batches(name, C, batch, lat_ctx):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("n,batch", [(4097, 2), (2000, 3), (513, 16)])
+def test_small_batches_two_level_fold(name, C, n, batch, lat_ctx):
+    """the one-launch kernel's two fold levels (more than 128 wavefront
+    partials per MSM) with per-MSM counters past the first MSM's"""
+    ctx = lat_ctx(name, C)
+    tau = K.default_tau(C)
+    polys = [K.random_scalars(C, n, seed=7400 + 13 * b + n) for b in range(batch)]
+    polys[-1][n // 2] = 0
+    out, inf = ctx.msm_batch(np.concatenate([limbs(P) for P in polys]), n, batch)
+    for b in range(batch):
+        assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, polys[b]), b
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("tau", [1, 2])
+def test_degenerate_setup_cooperative_levels(name, C, tau):
+    """tau = 1: every SRS point is G, so wavefront partials are small
+    multiples of G and the cooperative fold levels meet equal x (doubling)
+    and P = -Q; tau = 2 the same with distinct points"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(tau, 1600)
+        for n in (129, 1500):
+            P = [1] * n if tau == 1 else K.random_scalars(C, n, seed=7800 + n)
+            out, inf = ctx.msm(limbs(P))
+            assert pt(name, out, inf) == K.commit_via_tau(C, tau, P), n
+        P = [1, C.r - 1] * 700  # sums to zero
+        out, inf = ctx.msm(limbs(P))
+        assert pt(name, out, inf) == K.commit_via_tau(C, tau, P)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
 def test_single_proofs(name, C, lat_ctx):
     """create_proof(poly, z, 1) at degree 128 and 4096: quotient + table MSM"""
     ctx = lat_ctx(name, C)
@@ -127,5 +162,37 @@ def test_default_table_off_and_degenerate(name, C):
         outb, infb = ctx.msm_batch(np.concatenate([limbs(P[:90])] * 20), 90, 20)
         for b in range(20):
             assert pt(name, outb[b], infb[b]) == K.commit_via_tau(C, 0, P[:90]), b
+    finally:
+        ctx.close()
+
+
+def _quotient(C, P, z):
+    """synthetic division: q_(k-1) = h_k = sum_(i >= k) p_i z^(i - k), y = h_0"""
+    h, q = 0, [0] * max(len(P) - 1, 0)
+    for k in range(len(P) - 1, -1, -1):
+        h = (P[k] + h * z) % C.r
+        if k >= 1:
+            q[k - 1] = h
+    return q, h
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_single_opening_quotient_one_workgroup(name, C):
+    """create_proof(poly, z, 1) at the sizes of the one-workgroup quotient
+    (k_quotient_wg: 512 <= n <= 2^14, batch <= 4) and either side of it, with
+    full-width opening points: proof = [q(tau)]G1 and y = P(z)"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        tau = K.default_tau(C)
+        ctx.gen_srs(tau, 16400)
+        for n, batch in ((511, 1), (512, 1), (1025, 3), (4097, 4), (5000, 2), (16384, 1), (16385, 1)):
+            P = K.random_scalars(C, n, seed=7900 + n)
+            zs = K.random_scalars(C, batch, seed=7950 + n)
+            out, inf, y = ctx.prove_single_batch(limbs(P), limbs(zs))
+            for b in range(batch):
+                q, yv = _quotient(C, P, zs[b])
+                assert int(sum(int(y[b, i]) << (64 * i) for i in range(4))) == yv, (n, b)
+                assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, q), (n, b)
     finally:
         ctx.close()
