@@ -196,8 +196,8 @@ class trusted_setup {
   void precompute(int window_bits = 16, size_t points = 0);
   /** Extension: the default table (kzgx_set_default_table), built with
    *  every setup: odd multiples of the first 4097 SRS points at the widest
-   *  window c <= 12 that fits 2.5% of the HBM (window_bits = -1, the default:
-   *  BN254 c = 11, 6.4 GB; BLS12-381 c = 10, 6.1 GB).  Single create_commit /
+   *  window c <= 12 that fits 4.5% of the HBM (window_bits = -1, the default:
+   *  BN254 c = 12, 11.8 GB; BLS12-381 c = 11, 9.7 GB).  Single create_commit /
    *  create_proof calls of degree <= 4096 take its one-launch path, batches
    *  its batched kernel.  The reference's create_commit allocates nothing
    *  beyond the SRS (src/trusted_setup.cpp:137-142): default_table(0)

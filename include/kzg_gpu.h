@@ -109,9 +109,9 @@ int kzgx_set_fixed_base(kzgx_ctx* ctx, int c, size_t n_points);
 int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout);
 /* the default table (extension, no reference counterpart): odd multiples at
  * window c over the first n_points SRS points, built with every SRS load.
- * c = -1 (the default) picks the widest c <= 12 whose table fits 2.5% of the
+ * c = -1 (the default) picks the widest c <= 12 whose table fits 4.5% of the
  * device memory and its free memory less 4 GiB: over 4097 points BN254
- * c = 11 (6.4 GB), BLS12-381 c = 10 (6.1 GB) on an MI355X.  MSMs that fit in
+ * c = 12 (11.8 GB), BLS12-381 c = 11 (9.7 GB) on an MI355X.  MSMs that fit in
  * it and that the main table (kzgx_set_fixed_base) does not serve take it:
  * batches of at most kzgx_set_small_batch MSMs (single create_commit /
  * create_proof calls) its one-launch path, larger batches its batched

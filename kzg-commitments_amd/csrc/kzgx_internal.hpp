@@ -101,9 +101,9 @@ struct ProfRec {
 
 // the default table (Ctx::fixed_def): odd multiples of the first 4097 SRS
 // points (degree-4096 calls and below) at the widest window c <= 12 whose
-// table fits KZGX_DEFAULT_TABLE_PERMILLE of the device's memory -- 25 per
-// mille = 7.2 GB of an MI355X: BN254 c = 11 (6.4 GB), BLS12-381 c = 10
-// (6.1 GB).  -1 = that automatic choice, 0 = none, c = a fixed window.
+// table fits KZGX_DEFAULT_TABLE_PERMILLE of the device's memory -- 45 per
+// mille = 13 GB of an MI355X: BN254 c = 12 (11.8 GB), BLS12-381 c = 11
+// (9.7 GB).  -1 = that automatic choice, 0 = none, c = a fixed window.
 #ifndef KZGX_DEFAULT_TABLE_BITS
 #define KZGX_DEFAULT_TABLE_BITS -1
 #endif
@@ -111,7 +111,7 @@ struct ProfRec {
 #define KZGX_DEFAULT_TABLE_POINTS 4097
 #endif
 #ifndef KZGX_DEFAULT_TABLE_PERMILLE
-#define KZGX_DEFAULT_TABLE_PERMILLE 25
+#define KZGX_DEFAULT_TABLE_PERMILLE 45
 #endif
 // batches larger than Ctx::small_batch use the default table from this
 // window on (below it the batched Pippenger is as fast or faster).  cfg2

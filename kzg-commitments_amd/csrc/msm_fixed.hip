@@ -760,7 +760,10 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
     }
   }
   uint32_t P0 = ft.pts_per_thread;
-  if (P0 == 0) P0 = batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
+  // automatic: 16 points per thread from 64 MSMs (KZGX_PPT_AUTO_BIG: the
+  // count from 1024 MSMs, A/B), else enough threads to fill the chip
+  static const uint32_t ppt_big = std::getenv("KZGX_PPT_AUTO_BIG") ? (uint32_t)std::strtoul(std::getenv("KZGX_PPT_AUTO_BIG"), nullptr, 10) : 16u;
+  if (P0 == 0) P0 = batch >= 1024 && ppt_big ? ppt_big : batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
   uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
   // few large MSMs: 64:1 wavefront folds until at most 128 partials per MSM
   // remain, then one wavefront per MSM folds those and a thread per MSM

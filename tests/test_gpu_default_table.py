@@ -1,6 +1,6 @@
 """The default table (kzgx_set_default_table, Ctx::fixed_def): odd multiples
-over the first 4097 SRS points at the widest window c <= 12 that fits 2.5% of
-the HBM (BN254 c = 11, BLS12-381 c = 10 on an MI355X), built with the SRS,
+over the first 4097 SRS points at the widest window c <= 12 that fits 4.5% of
+the HBM (BN254 c = 12, BLS12-381 c = 11 on an MI355X), built with the SRS,
 read by the MSMs that fit in it -- every single create_commit / create_proof
 of degree <= 4096 (the reference's benchmark calls,
 benchmark/benchmark.cpp:40-66) through the one-launch path, larger batches
@@ -52,7 +52,7 @@ def test_default_table_is_built_by_default(name, C, lat_ctx):
     ctx = lat_ctx(name, C)
     c, n, b = ctx.default_table_info()
     total = torch.cuda.get_device_properties(0).total_memory
-    budget = total // 1000 * 25
+    budget = total // 1000 * 45
     assert n == 4097 and 7 <= c <= 12
     assert b == kzgx.fixed_base_bytes(name, c, 4097) <= budget
     if c < 12:  # the widest that fits (the free-memory cap aside)
