@@ -853,9 +853,10 @@ __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW
 // U (wave-uniform): the caller guarantees the first active lane holds the
 // value every lane needs -- a single lane's tail (lane 0 of the latency
 // path's fold) -- and the input is read from that lane, so the whole GCD
-// state is uniform and runs on the scalar ALU: one SALU instruction per
-// clock where a lone wave's dependent VALU instruction costs ~8.  Never with
-// a different value per lane (the batched finish kernels).
+// state is uniform: the bit-serial inner loop runs on the scalar ALU, and
+// with lanes 0-3 active the four linear combinations of a pass run one per
+// lane (combine4).  Never with a different value per lane (the batched
+// finish kernels).
 template <class F, int NW, bool U = false>
 __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[NW]) {
   constexpr int L = F::L;
@@ -929,6 +930,51 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[
     }
     return f29_csub<F>(r, F::P);
   };
+  // U: lane k < 4 computes one of a' = |a f0 + b g0| / 2^29 (k = 0),
+  // b' = |a f1 + b g1| / 2^29 (1), u' = (u f0 + v g0) / 2^29 mod m (2),
+  // v' = (u f1 + v g1) / 2^29 mod m (3) -- the exact division and the
+  // Montgomery halving as one routine (q = 0 on lanes 0 and 1) -- then lanes
+  // 2 and 3 take the sign of lanes 0 and 1 (x -> m - x), and the four
+  // results return to uniform registers (readlane)
+  auto combine4 = [](F29<F>& a, F29<F>& b, F29<F>& u, F29<F>& v, int32_t f0, int32_t g0, int32_t f1, int32_t g1) {
+    const uint32_t lane = __lane_id();
+    const bool hi = (lane & 1) != 0, md = (lane & 2) != 0;
+    const int32_t f = hi ? f1 : f0, g = hi ? g1 : g0;
+    F29<F> r;
+    int64_t c = (int64_t)(int32_t)(md ? u.v[0] : a.v[0]) * f + (int64_t)(int32_t)(md ? v.v[0] : b.v[0]) * g;
+    const uint32_t q = md ? ((uint32_t)c * F::INV) & M29 : 0u;
+    c += (int64_t)q * F::P[0];
+    c >>= K;
+#pragma unroll
+    for (int j = 1; j < L; j++) {
+      c += (int64_t)(int32_t)(md ? u.v[j] : a.v[j]) * f + (int64_t)(int32_t)(md ? v.v[j] : b.v[j]) * g +
+           (int64_t)q * F::P[j];
+      r.v[j - 1] = (uint32_t)c & M29;
+      c >>= K;
+    }
+    r.v[L - 1] = (uint32_t)c;
+    const bool neg = c < 0;
+    // negative: lanes 0, 1 take |r| = -r, lanes 2, 3 add m (r in (-m, 2m))
+    int64_t d = 0;
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      const int64_t rj = (int64_t)(int32_t)r.v[j];
+      d += neg ? (md ? rj + (int64_t)F::P[j] : -rj) : rj;
+      r.v[j] = j + 1 < L ? (uint32_t)d & M29 : (uint32_t)d;
+      d >>= K;
+    }
+    if (md) r = f29_csub<F>(r, F::P);  // [0, m)
+    // lanes 2, 3: the sign lanes 0, 1 folded into f, g in the per-lane form
+    const int sgn = __shfl((int)neg, (int)(lane & 1), 64);
+    if (md && sgn && !f29_is_zero_exact<F>(r)) r = f29_sub<F>(f29_zero<F>(), r, F::P);  // m - r
+#pragma unroll
+    for (int j = 0; j < L; j++) {
+      a.v[j] = __builtin_amdgcn_readlane(r.v[j], 0);
+      b.v[j] = __builtin_amdgcn_readlane(r.v[j], 1);
+      u.v[j] = __builtin_amdgcn_readlane(r.v[j], 2);
+      v.v[j] = __builtin_amdgcn_readlane(r.v[j], 3);
+    }
+  };
   // 3x the most passes seen: a bound every lane reaches even on a bad input
   for (int pass = 0; pass < 3 * (2 * 29 * L / K + 2) && !f29_is_zero_exact<F>(a); pass++) {
     // n = max(len(a), len(b), 60); the approximations keep bits [0, 29) and
@@ -970,6 +1016,16 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[
       f1 = (int32_t)((uint32_t)f1 << z);
       g1 = (int32_t)((uint32_t)g1 << z);
       rem -= z;
+    }
+    if constexpr (U) {
+      // the four combinations side by side, one per lane (lanes 0-3), in one
+      // instruction stream -- a lone wave pays per instruction, not per lane
+      // -- when lanes 0-3 are active (callers from a one-thread region fall
+      // through to the sequential form)
+      if ((__builtin_amdgcn_read_exec() & 0xFull) == 0xFull) {
+        combine4(a, b, u, v, f0, g0, f1, g1);
+        continue;
+      }
     }
     F29<F> a2, b2;
     if (combine(a, b, f0, g0, a2)) {

@@ -573,13 +573,24 @@ __global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* 
   __syncthreads();
   if (l < 2) U = xyzz_add_impl<C>(xyzz_load<C>(lds + l * XW), xyzz_load<C>(lds + (l + 2) * XW));
   U = xyzz_add_impl<C>(U, xyzz_shfl_down<C>(U, 1));
-  if (l != 0) return;
+  if (wv != 0) return;  // wavefront 0 (the sum in its lane 0) converts
   if (xyzz_out) {
-    xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
+    if (l == 0) xyzz_store<C>(xyzz_out + (size_t)b * XW, U);
     return;
   }
+  // the whole wavefront on lane 0's value: the inversion's loop on the scalar
+  // ALU, its linear combinations one per lane (f29_inv_uniform)
+  Xyzz<C> s;
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++) {
+    s.X.v[k] = __builtin_amdgcn_readfirstlane(U.X.v[k]);
+    s.Y.v[k] = __builtin_amdgcn_readfirstlane(U.Y.v[k]);
+    s.ZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZ.v[k]);
+    s.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZZ.v[k]);
+  }
   Affine<C> a;
-  const bool fin = xyzz_to_affine_lane<C>(U, a);  // thread 0 alone: scalar-ALU inversion
+  const bool fin = xyzz_to_affine_lane<C>(s, a);
+  if (l != 0) return;
   affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
   out_inf[b] = fin ? 0u : 1u;
 }

@@ -406,13 +406,23 @@ KZGX_DEV Xyzz<C> lat_fold(const uint32_t* __restrict__ p, uint32_t Q, uint32_t l
   return acc;
 }
 
-// lane 0 converts MSM b's sum and stores it (its inversion on the scalar ALU)
+// MSM b's sum (lane 0's) converted by the whole wavefront on lane 0's value
+// (uniform: the inversion's bit-serial loop on the scalar ALU, its linear
+// combinations one per lane) and stored by lane 0
 template <class C>
 KZGX_DEV void lat_store_affine(const Xyzz<C>& acc, uint32_t b, uint32_t lane, uint32_t* __restrict__ out,
                                uint32_t* __restrict__ out_inf) {
+  Xyzz<C> s;
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++) {
+    s.X.v[k] = __builtin_amdgcn_readfirstlane(acc.X.v[k]);
+    s.Y.v[k] = __builtin_amdgcn_readfirstlane(acc.Y.v[k]);
+    s.ZZ.v[k] = __builtin_amdgcn_readfirstlane(acc.ZZ.v[k]);
+    s.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(acc.ZZZ.v[k]);
+  }
+  Affine<C> a;
+  const bool fin = xyzz_to_affine_lane<C>(s, a);
   if (lane == 0) {
-    Affine<C> a;
-    const bool fin = xyzz_to_affine_lane<C>(acc, a);
     affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
     out_inf[b] = fin ? 0u : 1u;
   }
@@ -760,10 +770,17 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
     }
   }
   uint32_t P0 = ft.pts_per_thread;
-  // automatic: 16 points per thread from 64 MSMs (KZGX_PPT_AUTO_BIG: the
-  // count from 1024 MSMs, A/B), else enough threads to fill the chip
-  static const uint32_t ppt_big = std::getenv("KZGX_PPT_AUTO_BIG") ? (uint32_t)std::strtoul(std::getenv("KZGX_PPT_AUTO_BIG"), nullptr, 10) : 16u;
-  if (P0 == 0) P0 = batch >= 1024 && ppt_big ? ppt_big : batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
+  // automatic: 16 points per thread from 64 MSMs; BLS12-381 from 2048 MSMs
+  // 65 (one residency at two waves per SIMD, the cfg4 shape: +2.4% on the
+  // default table's batches, profiles/r04_ab_ppt_auto.json; BN254 22 vs 16
+  // measured +0.3%, kept); else enough threads to fill the chip.
+  // KZGX_PPT_AUTO_BIG: the count from 1024 MSMs (A/B)
+  static const uint32_t ppt_env = std::getenv("KZGX_PPT_AUTO_BIG") ? (uint32_t)std::strtoul(std::getenv("KZGX_PPT_AUTO_BIG"), nullptr, 10) : 0u;
+  if (P0 == 0) {
+    if (ppt_env && batch >= 1024) P0 = ppt_env;
+    else if (C::Fp29::L > 9 && batch >= 2048) P0 = 65;
+    else P0 = batch >= 64 ? 16u : (uint32_t)std::max<size_t>(1, (n * batch + kSlots - 1) / kSlots);
+  }
   uint32_t T = (uint32_t)(64 * ((n + 64 * (size_t)P0 - 1) / (64 * (size_t)P0)));
   // few large MSMs: 64:1 wavefront folds until at most 128 partials per MSM
   // remain, then one wavefront per MSM folds those and a thread per MSM
@@ -1047,14 +1064,15 @@ int microbench_mixed_add(Ctx* ctx, double* rate) {
 // (no launch overhead).  op: 0 Montgomery product, 1 Fermat inversion,
 // 2 binary-Euclid inversion, 3 XYZZ addition, 4 mixed addition, 5 XYZZ ->
 // affine conversion, 6 / 7 the same as 2 / 5 on the scalar ALU (one lane's
-// value made wave-uniform).
+// value made wave-uniform), 8 / 9 the same with the whole wavefront active
+// (the linear combinations one per lane).
 // --------------------------------------------------------------------------
 template <class C>
 __global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict__ pts, int op, uint32_t iters,
                                                       uint64_t* __restrict__ out) {
   using F = typename C::Fp29;
   constexpr int PW = affine_words<C>();
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x != 0 && op < 8) return;  // 8, 9: the whole wavefront on one value
   const Affine<C> p = affine_load<C>(pts), q = affine_load<C>(pts + PW);
   F29<F> a = p.x;
   Xyzz<C> acc = xyzz_from_affine<C>(p);
@@ -1067,8 +1085,8 @@ __global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict
     else if (op == 2) a = f29_inv_vt<F, C::Fp::N>(a, C::Fp::P);
     else if (op == 3) acc = xyzz_add_impl<C>(acc, qx);
     else if (op == 4) acc = xyzz_add_affine_impl<C>(acc, q);
-    else if (op == 6) a = f29_inv_uniform<F, C::Fp::N>(a, C::Fp::P);
-    else if (op == 7) {
+    else if (op == 6 || op == 8) a = f29_inv_uniform<F, C::Fp::N>(a, C::Fp::P);
+    else if (op == 7 || op == 9) {
       Affine<C> r;
       (void)xyzz_to_affine_impl<C, true>(acc, r);
       acc.X = r.y;
@@ -1082,6 +1100,7 @@ __global__ __launch_bounds__(64) void k_debug_latency(const uint32_t* __restrict
   uint32_t o = 0;
 #pragma unroll
   for (int i = 0; i < F::L; i++) o ^= a.v[i] ^ acc.X.v[i] ^ acc.ZZ.v[i];
+  if (threadIdx.x != 0) return;
   out[0] = w1 - w0;
   out[1] = c1 - c0;
   out[2] = o;
@@ -1116,7 +1135,7 @@ static int debug_latency_impl(Ctx* ctx, int op, uint32_t iters, double* res) {
 }
 
 int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res) {
-  if (op < 0 || op > 7 || iters == 0) return KZGX_ERR_ARG;
+  if (op < 0 || op > 9 || iters == 0) return KZGX_ERR_ARG;
   return ctx->curve == KZGX_CURVE_BN254 ? debug_latency_impl<BN254G1>(ctx, op, iters, res)
                                         : debug_latency_impl<BLS12381G1>(ctx, op, iters, res);
 }

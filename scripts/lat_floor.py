@@ -28,6 +28,8 @@ def med(f, reps=15):
 
 C = K.BN254
 ctx = kzgx.Context("BN254")
+if os.environ.get("LAT_NO_DEFAULT_TABLE"):  # the table-off (Pippenger) path
+    ctx.set_default_table(0)
 ctx.gen_srs(K.default_tau(C), 5000)
 P = np.array([[(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)] for v in K.random_scalars(C, 4097, 5)],
              dtype=np.uint64)

@@ -13,7 +13,8 @@ import kzg_ref as K  # noqa: E402
 lib = kzgx.lib()
 lib.kzgx_debug_latency.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint, ctypes.POINTER(ctypes.c_double)]
 OPS = [("mont_mul", 4000), ("inv_fermat", 40), ("inv_euclid", 40), ("xyzz_add", 400), ("mixed_add", 400),
-       ("to_affine", 40), ("inv_euclid_salu", 40), ("to_affine_salu", 40)]
+       ("to_affine", 40), ("inv_euclid_salu", 40), ("to_affine_salu", 40),
+       ("inv_euclid_wave", 40), ("to_affine_wave", 40)]
 for name, C in [("BN254", K.BN254), ("BLS12381", K.BLS12381)]:
     ctx = kzgx.Context(name, device=0)
     ctx.gen_srs(K.default_tau(C), 4)
