@@ -704,7 +704,16 @@ static int fixed_msm_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, s
     static const size_t lat_threads = std::getenv("KZGX_LAT_THREADS") ? std::strtoul(std::getenv("KZGX_LAT_THREADS"), nullptr, 10) : 16384;
     const size_t per_msm = std::max<size_t>(std::min<size_t>(lat_threads, 16384), lat_threads / batch);
     int G = (int)std::min<size_t>(W, std::max<size_t>(1, per_msm / n_pad));
-    const int WG = (W + G - 1) / G;
+    int WG = (W + G - 1) / G;
+    // between 64 and 128 partials, one more window per thread when that
+    // leaves <= 64 partials (a fold with no strided level: a mixed addition
+    // instead of an XYZZ one on the chain; degree 128 / 256 commits -2.5 us,
+    // profiles/r04_lat_ab_q64_qwg8.txt; KZGX_LAT_Q64=0 turns it off, A/B)
+    static const bool q64 = !(std::getenv("KZGX_LAT_Q64") && std::getenv("KZGX_LAT_Q64")[0] == '0');
+    if (q64 && n_pad * G / 64 > 64 && n_pad * G / 64 <= 128) {
+      const int G2 = (int)(64 * 64 / n_pad);
+      if (G2 >= 1 && (W + G2 - 1) / G2 <= WG + 1) WG = (W + G2 - 1) / G2;
+    }
     G = (W + WG - 1) / WG;
     const uint32_t Q = (uint32_t)(n_pad * G / 64);
     const uint32_t NG = Q > 128 ? (Q + 63) / 64 : 1;  // <= 16

@@ -133,10 +133,9 @@ __global__ __launch_bounds__(256) void k_quotient_single(const uint32_t* __restr
 //   wavefront totals H_w through LDS, each wavefront scanning them itself
 //   (log2 NWV steps, multiplier Z = z^(64 L), the scan's last power) into
 //   C_w = h at the top of wavefront w and y = h_0; carry-in c_{t+1} + C_w pw;
-//   replay.  NWV = 4: one wavefront per SIMD of the CU -- a lone wavefront
-//   issues every cycle its SIMD offers, 16 would share each SIMD four ways
-//   and run every product of the chain 4x slower (measured: 1024 threads lost
-//   to the chip-wide kernel).
+//   replay.  NWV = 8 (two wavefronts per SIMD of the CU) by default: 4 is one
+//   per SIMD with twice the chunk (9 us slower at degree 4096), 16 shares each
+//   SIMD four ways and lost to the chip-wide kernel outright.
 template <class FR, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_quotient_wg(const uint32_t* __restrict__ coeffs, uint32_t n,
                                                           size_t cstride, const uint32_t* __restrict__ zs,
@@ -455,8 +454,16 @@ static int quotient_single_impl(Ctx* ctx, const uint32_t* d_coeffs, size_t n, si
     return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)512;
   }();
   if (batch <= 4 && QWG_MIN && n >= QWG_MIN && n <= (1u << 14)) {
-    hipLaunchKernelGGL((k_quotient_wg<FR, 4>), dim3((unsigned)batch), dim3(256), 0, st, d_coeffs, (uint32_t)n, cstride,
-                       d_z, d_q, qstride, d_y);
+    // 8 wavefronts (two per SIMD, half the chunk length): degree-4096 proof
+    // -9 us against 4 (profiles/r04_lat_ab_q64_qwg8.txt); KZGX_QWG_WAVES=4
+    // selects 4 (A/B)
+    static const bool w8 = !(std::getenv("KZGX_QWG_WAVES") && std::strtoul(std::getenv("KZGX_QWG_WAVES"), nullptr, 10) == 4);
+    if (w8)
+      hipLaunchKernelGGL((k_quotient_wg<FR, 8>), dim3((unsigned)batch), dim3(512), 0, st, d_coeffs, (uint32_t)n,
+                         cstride, d_z, d_q, qstride, d_y);
+    else
+      hipLaunchKernelGGL((k_quotient_wg<FR, 4>), dim3((unsigned)batch), dim3(256), 0, st, d_coeffs, (uint32_t)n,
+                         cstride, d_z, d_q, qstride, d_y);
     KZGX_TRY_HIP(hipGetLastError());
     return KZGX_OK;
   }
