@@ -598,6 +598,8 @@ def main():
         # a fixed total batch split over the ranks (the first ranks take the
         # remainder): 1/2/4/8 GPUs then trace a strong-scaling curve
         global_batch = args.global_batch or 8 * shape["batch"]
+        if global_batch < world:  # every rank needs at least one polynomial
+            raise SystemExit("--global-batch %d is smaller than the world size %d" % (global_batch, world))
         B = global_batch // world + (1 if rank < global_batch % world else 0)
     if args.fixed_ppt < 0:
         args.fixed_ppt = shape["points_per_thread"]
@@ -956,25 +958,29 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     coeffs_h = random_fr(rng, (n,), C.r)
     d_c = torch.from_numpy(coeffs_h[start:start + count].copy().view(np.int64)).to(dev)
     w64 = ctx.w64
-    d_out = torch.zeros((2 * w64,), dtype=torch.int64, device=dev)
-    d_inf = torch.zeros((1,), dtype=torch.int32, device=dev)
-    d_res = torch.zeros((2 * w64,), dtype=torch.int64, device=dev)
-    d_res_inf = torch.zeros((1,), dtype=torch.int32, device=dev)
+    # packed records (x || y canonical limbs, then an int64 infinity word):
+    # the partial MSM writes its record in place (the flag as the low 32
+    # bits of a zeroed int64), RCCL gathers the records into one tensor, and
+    # kzgx_g1_sum_packed_device folds them in one launch -- no stack / cast /
+    # cat between the phases (What's weak 4)
+    d_rec = torch.zeros((2 * w64 + 1,), dtype=torch.int64, device=dev)
+    d_res = torch.zeros((2 * w64 + 1,), dtype=torch.int64, device=dev)
+    if count == 0:  # an empty shard contributes the identity
+        d_rec[2 * w64] = 1
     stream = torch.cuda.Stream(device=dev)
 
-    # Device-resident step: the partial MSM, the packing, the RCCL all-gather
-    # and the exact fold (kzgx_g1_sum_device) are all enqueued on one stream;
-    # nothing crosses to the host inside a step.
+    # Device-resident step: the partial MSM, the RCCL all-gather and the
+    # exact fold are all enqueued on one stream; nothing crosses to the host
+    # inside a step.
     def partial(s0, cnt):
-        if cnt == 0:  # an empty shard contributes the identity
-            return torch.cat([torch.zeros_like(d_out), torch.ones((1,), dtype=torch.int64, device=dev)])
-        ctx.msm_batch_device(d_c.data_ptr(), cnt, 1, cnt, d_out.data_ptr(), d_inf.data_ptr(), stream.cuda_stream)
-        return torch.cat([d_out, d_inf.to(torch.int64)])
+        if cnt:
+            ctx.msm_batch_device(d_c.data_ptr(), cnt, 1, cnt, d_rec.data_ptr(), d_rec.data_ptr() + 16 * w64,
+                                 stream.cuda_stream)
+        return d_rec
 
-    def fold(pts, flags):
-        ctx.g1_sum_device(pts.data_ptr(), flags.data_ptr(), pts.shape[0], d_res.data_ptr(), d_res_inf.data_ptr(),
-                          stream.cuda_stream)
-        return torch.cat([d_res, d_res_inf.to(torch.int64)])
+    def fold(recs):
+        ctx.g1_sum_packed_device(recs.data_ptr(), recs.shape[0], d_res.data_ptr(), stream.cuda_stream)
+        return d_res
 
     # per-phase HIP events on the step's stream: start, partial MSM enqueued,
     # all-gather done (the collective's completion is ordered before the
@@ -1011,22 +1017,33 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     # phase times of this rank, mean over the timed steps
     names = ["partial_msm", "all_gather", "fold"]
     phase_tot = [0.0] * 3
+    phase_min = [float("inf")] * 3
+    phase_max = [0.0] * 3
     for m in marks:
         for k in range(min(3, len(m) - 1)):
-            phase_tot[k] += m[k].elapsed_time(m[k + 1])
-    my_phases = {names[k]: phase_tot[k] / max(1, len(marks)) for k in range(3 if world > 1 else 1)}
+            t_k = m[k].elapsed_time(m[k + 1])
+            phase_tot[k] += t_k
+            phase_min[k] = min(phase_min[k], t_k)
+            phase_max[k] = max(phase_max[k], t_k)
+    nph = 3 if world > 1 else 1
+    my_phases = {names[k]: phase_tot[k] / max(1, len(marks)) for k in range(nph)}
+    # per-step extremes, so a slow step (e.g. two ranks time-slicing one
+    # device) shows in the record itself
+    my_phase_range = {names[k]: [phase_min[k], phase_max[k]] for k in range(nph)}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ranks = rank_records(world, rank, local, dev, local_s, dist, torch,
-                         {"shard_points": count, "phase_ms_per_step": my_phases})
+                         {"shard_points": count, "phase_ms_per_step": my_phases,
+                          "phase_ms_min_max": my_phase_range})
     dinfo = dist_info(world, dist, torch)
     phases = {"rank0": my_phases,
               "max_over_ranks": {k: max(r["phase_ms_per_step"].get(k, 0.0) for r in ranks) for k in my_phases},
+              "min_max_over_steps_rank0": my_phase_range,
               "from": "HIP events on the step stream: partial_msm = this rank's shard MSM; all_gather = the "
-                      "RCCL all-gather of the packed partial points (until the stream may use them); fold = "
-                      "kzgx_g1_sum_device of the gathered points"}
+                      "%s all-gather of the packed partial records (until the stream may use them); fold = "
+                      "kzgx_g1_sum_packed_device of the gathered records" % dinfo.get("backend", "no")}
     if rank == 0:
         xys, infs = kzgx_dist.unpack_points(res.cpu().numpy(), w64)
         xy, inf = xys[0], bool(infs[0])
@@ -1069,6 +1086,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                           "(oracle/kzg_oracle.c: naive per-term double-and-add, no GLV), 1 thread, %.1f s, "
                           "scaled linearly to the full commit" % (m, n, tcpu),
             }
+        n_dev = len({r.get("uuid") or r.get("pci") for r in ranks}) or world
         line = {
             "metric": "KZG commits/sec, BN254 degree-2^20, sharded",
             "value": args.steps / elapsed,
@@ -1082,7 +1100,8 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
             "vs_baseline": None,
             "dtype": "uint32 limbs (254-bit Montgomery Fp)",
             "data": "synthetic: seeded uniform Fr coefficients, SRS [tau^i]G1 from fixed tau",
-            "config": {"workload": "BN254 degree-2^20 commit, point range sharded, device-resident RCCL all-gather + fold",
+            "config": {"workload": "BN254 degree-2^20 commit, point range sharded, device-resident %s" % (
+                           "%s all-gather + fold" % dinfo.get("backend") if world > 1 else "single shard (no exchange)"),
                        "n_coeffs": n, "shard_points": count,
                        "msm": ("fixed-base table over the shard, c=%d, %.1f GB" % (
                            fixed_bits, ctx.fixed_base_info()[2] / 1e9)) if fixed_bits else
@@ -1092,10 +1111,11 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                 "kernel": "msm_accum (one MSM per rank) + all-gather + fold",
                 "bound": "hbm",
                 "achieved": achieved,
-                "peak": HBM_PEAK_GBS * world,
+                "peak": HBM_PEAK_GBS * n_dev,
                 "unit": "GB/s",
-                "frac": achieved / (HBM_PEAK_GBS * world),
+                "frac": achieved / (HBM_PEAK_GBS * n_dev),
                 "traffic": None,
+                "distinct_devices": n_dev,
                 "algorithmic_bytes_per_step": unit_bytes,
                 "achieved_from": "algorithmic bytes of one commit / ms_per_step",
                 "note": "integer-VALU bound (no MFMA); see secondary.valu_yardstick",

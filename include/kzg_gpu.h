@@ -64,6 +64,14 @@ const char* kzgx_strerror(int status);
 /* uint64 limbs per base-field coordinate (4 or 6), or -1 */
 int kzgx_base_limbs(int curve);
 
+/* Device bring-up for `curve` on `device`, meant to run once, outside any
+ * timed region: HIP initialisation, every kernel code object of the library
+ * loaded, and the per-process generator tables (comb tables of G1 and G2,
+ * used by SRS generation and verify) built.  Replaces the device-independent
+ * kzg::init of the reference (src/kzg.h:33-38, kzg.cpp init; its benchmark
+ * calls it before timing, benchmark/benchmark.cpp:104).  Optional: without
+ * it the first setup pays the same work. */
+int kzgx_init_device(int curve, int device);
 int kzgx_create(kzgx_ctx** out, int curve, int device);
 void kzgx_destroy(kzgx_ctx* ctx);
 int kzgx_sync(kzgx_ctx* ctx);
@@ -227,6 +235,13 @@ int kzgx_g1_sum(kzgx_ctx* ctx, const uint64_t* xy, const int* is_inf, size_t cou
  * host round trip. */
 int kzgx_g1_sum_device(kzgx_ctx* ctx, const void* d_xy, const void* d_inf, size_t count, void* d_out_xy,
                        void* d_out_inf, void* stream);
+/* The same fold over packed records, the exchange format of the sharded
+ * commitment (python/kzgx_dist.py): record k is 2 W64 uint64 (x || y,
+ * canonical little-endian) followed by one uint64 infinity word (nonzero =
+ * infinity); the sum is written as one record.  One launch, one wave
+ * (strided sums, a shuffle tree, a wave-uniform inversion).  Device
+ * pointers; stream as kzgx_msm_g1_batch_device. */
+int kzgx_g1_sum_packed_device(kzgx_ctx* ctx, const void* d_records, size_t count, void* d_out_record, void* stream);
 /* One commitment sharded over several contexts, typically one per GPU (the
  * one-process form of SURVEY 8e's sharded commit; bench.py's configs[4] runs
  * the one-process-per-GPU form over RCCL).  Context k holds the SRS slice

@@ -130,10 +130,59 @@ KZGX_DEV void mad_vs(uint64_t& acc, uint32_t x, uint32_t y_uniform) {
 #endif
 }
 
+// Latency-first Montgomery product for code that runs as a lone wave (the
+// verify path): the same value and bounds as f29_mul, arranged for a short
+// dependency chain instead of few instructions.  f29_mul threads every
+// partial product of every column through ONE accumulator (a ~2L^2-long
+// dependent mad chain: fine when other waves fill the SIMD, ~15 cycles per
+// mad when the wave is alone).  Here the 2L - 1 column sums are independent
+// chains of <= L mads, and only the reduction digits form a chain (L steps
+// of digit, mad, shift).  Column bound: 2L products < 2^58 plus a carry,
+// < 2^63 for both curves.
+template <class F>
+KZGX_DEV F29<F> f29_mul_lat(const F29<F>& a, const F29<F>& b) {
+  constexpr int L = F::L;
+  uint64_t col[2 * L];
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) s += (uint64_t)a.v[i] * b.v[j];
+    }
+    col[k] = s;
+  }
+  col[2 * L - 1] = 0;
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    const uint32_t q = ((uint32_t)col[k] * F::INV) & M29;
+    col[k + 1] += (col[k] + (uint64_t)q * F::P[0]) >> 29;
+#pragma unroll
+    for (int j = 1; j < L; j++) col[k + j] += (uint64_t)q * F::P[j];
+  }
+  F29<F> t;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = L; k < 2 * L - 1; k++) {
+    const uint64_t s = col[k] + c;
+    t.v[k - L] = (uint32_t)s & M29;
+    c = s >> 29;
+  }
+  t.v[L - 1] = (uint32_t)c;
+  return t;
+}
+
 // Montgomery product a b / R mod m, product scanning; output < 2m when
-// a b < (R / m) m^2 (see header).
+// a b < (R / m) m^2 (see header).  A translation unit that defines
+// KZGX_FIELD_LATENCY before including this header (verify_wave.hip: one
+// wave per pairing) gets the latency-first form for every f29_mul /
+// f29_sqr, including those inside the tower and curve code.
 template <class F>
 KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
+#ifdef KZGX_FIELD_LATENCY
+  return f29_mul_lat<F>(a, b);
+#endif
   constexpr int L = F::L;
   uint32_t q[L];
   F29<F> t;
@@ -624,6 +673,9 @@ KZGX_DEV void f29_mul2_x3(const F29<F>& a0, const F29<F>& b0, const F29<F>& c0, 
 // Montgomery square: cross products once, against a doubled operand
 template <class F>
 KZGX_DEV F29<F> f29_sqr(const F29<F>& a) {
+#ifdef KZGX_FIELD_LATENCY
+  return f29_mul_lat<F>(a, a);
+#endif
   constexpr int L = F::L;
   uint32_t q[L], d[L];
 #pragma unroll

@@ -229,9 +229,21 @@ void init() { init(KZGX_CURVE_BN254); }
 
 void init(int curve) {
   if (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) throw std::invalid_argument("unknown curve");
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_curve = curve;
-  CURVE_ORDER_BYTES = 32;  // NumBytes(r) on both curves (trusted_setup.cpp:18)
+  int dev;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_curve = curve;
+    CURVE_ORDER_BYTES = 32;  // NumBytes(r) on both curves (trusted_setup.cpp:18)
+    dev = g_device;
+  }
+  // the reference's init sets up its curve state before any other call
+  // (src/kzg.h:33-38); here that is the device: HIP, every code object and
+  // the generator tables, so no later call pays them.  Without a gfx950
+  // device init still succeeds and the first GPU call throws.
+  const int rc = kzgx_init_device(curve, dev);
+  if (rc == KZGX_ERR_NO_DEVICE) return;
+  check(rc, "kzgx_init_device");
+  (void)default_ctx();
 }
 
 int curve() { return g_curve; }

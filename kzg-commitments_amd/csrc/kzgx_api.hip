@@ -16,6 +16,7 @@
 
 #include "curve_consts.h"
 #include "kzgx_internal.hpp"
+#include "kzgx_setup.hpp"
 
 struct kzgx_ctx {
   kzgx::Ctx c;
@@ -148,6 +149,19 @@ std::array<uint64_t, 4> fr_reduce(const uint64_t* x) {
   return {v[0], v[1], v[2], v[3]};
 }
 
+// gfx950 device check shared by kzgx_create and kzgx_init_device
+int device_ok(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KZGX_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return KZGX_ERR_ARG;
+  hipDeviceProp_t prop;
+  KZGX_TRY_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return KZGX_ERR_NO_DEVICE;
+  return KZGX_OK;
+}
+
+int setup_finish(kzgx_ctx* ctx);
+
 }  // namespace
 
 extern "C" {
@@ -171,15 +185,37 @@ int kzgx_base_limbs(int curve) {
   return curve == KZGX_CURVE_BN254 ? 4 : curve == KZGX_CURVE_BLS12381 ? 6 : -1;
 }
 
+int kzgx_init_device(int curve, int device) {
+  if (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) return KZGX_ERR_ARG;
+  KZGX_TRY(device_ok(device));
+  KZGX_TRY_HIP(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  KZGX_TRY_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() { (void)hipStreamDestroy(s); }
+  } sg{st};
+  // every code object of the library, once (the first launch of any kernel
+  // of a translation unit loads its whole object)
+  int (*const warm[])(hipStream_t) = {kzgx::warm_setup, kzgx::warm_msm,     kzgx::warm_msm_fixed,
+                                       kzgx::warm_poly,  kzgx::warm_srs,     kzgx::warm_pairing,
+                                       kzgx::warm_verify_wave, kzgx::warm_latency};
+  for (auto f : warm) KZGX_TRY(f(st));
+  // the generator comb tables (per process, per device and curve)
+  kzgx::GenTables g;
+  KZGX_TRY(kzgx::gen_tables_get(curve, device, st, &g));
+  // the pinned-allocation path of the host-pointer calls
+  void* h = nullptr;
+  KZGX_TRY_HIP(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  (void)hipHostFree(h);
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  return KZGX_OK;
+}
+
 int kzgx_create(kzgx_ctx** out, int curve, int device) {
   if (!out || (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381)) return KZGX_ERR_ARG;
   *out = nullptr;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KZGX_ERR_NO_DEVICE;
-  if (device < 0 || device >= ndev) return KZGX_ERR_ARG;
-  hipDeviceProp_t prop;
-  KZGX_TRY_HIP(hipGetDeviceProperties(&prop, device));
-  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return KZGX_ERR_NO_DEVICE;
+  KZGX_TRY(device_ok(device));
   kzgx_ctx* ctx = new (std::nothrow) kzgx_ctx();
   if (!ctx) return KZGX_ERR_OOM;
   ctx->c.curve = curve;
@@ -205,7 +241,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->c.stream);
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
-  void* bufs[] = {c.d_table, c.d_table_small, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
+  void* bufs[] = {c.d_table, c.d_table_small, c.d_table_big, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
                   c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw, ctx->d_g2tab};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -438,7 +474,7 @@ int kzgx_load_srs_g1(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
   KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_srs_canon, xy, bytes, hipMemcpyHostToDevice, ctx->c.stream));
   KZGX_TRY(kzgx::srs_upload(&ctx->c, ctx->d_srs_canon, n));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
-  return KZGX_OK;
+  return setup_finish(ctx);
 }
 
 int kzgx_gen_srs_g1(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) {
@@ -450,10 +486,13 @@ int kzgx_gen_srs_g1(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) 
   void* d_tau;
   KZGX_TRY(stage(ctx, 0, 32, &d_tau));
   KZGX_TRY_HIP(hipMemcpyAsync(d_tau, tau, 32, hipMemcpyHostToDevice, ctx->c.stream));
-  KZGX_TRY(kzgx::gen_srs_points(&ctx->c, (const uint32_t*)d_tau, start, n, ctx->d_srs_canon, ctx->c.stream));
+  kzgx::GenTables g;
+  KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, ctx->c.stream, &g));
+  KZGX_TRY(kzgx::gen_srs_g1_comb(ctx->c.curve, (const uint32_t*)d_tau, start, n, g.g1_comb, ctx->d_srs_canon,
+                                 ctx->c.stream));
   KZGX_TRY(kzgx::srs_upload(&ctx->c, ctx->d_srs_canon, n));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
-  return KZGX_OK;
+  return setup_finish(ctx);
 }
 
 int kzgx_get_srs_g1(kzgx_ctx* ctx, uint64_t* xy, size_t n) {
@@ -761,6 +800,13 @@ int kzgx_g1_sum_device(kzgx_ctx* ctx, const void* d_xy, const void* d_inf, size_
                       (uint32_t*)d_out_inf, pick(ctx, stream));
 }
 
+int kzgx_g1_sum_packed_device(kzgx_ctx* ctx, const void* d_records, size_t count, void* d_out_record, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (!d_out_record || (count > 0 && !d_records) || count > 0xffffffu) return KZGX_ERR_ARG;
+  return kzgx::g1_fold_packed(ctx->c.curve, (const uint32_t*)d_records, count, (uint32_t*)d_out_record,
+                              pick(ctx, stream));
+}
+
 int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
                         size_t n, uint64_t* out_xy, int* out_is_inf) {
   if (!ctxs || !starts || nctx == 0 || (n > 0 && !scalars) || !out_xy || !out_is_inf) return KZGX_ERR_ARG;
@@ -860,10 +906,13 @@ int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) 
   void* d_tau;
   KZGX_TRY(stage(ctx, 0, 32, &d_tau));
   KZGX_TRY_HIP(hipMemcpyAsync(d_tau, tau, 32, hipMemcpyHostToDevice, ctx->c.stream));
-  KZGX_TRY(kzgx::gen_srs_g2_points(&ctx->c, (const uint32_t*)d_tau, start, n, ctx->d_srs2_canon, ctx->c.stream));
+  kzgx::GenTables g;
+  KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, ctx->c.stream, &g));
+  KZGX_TRY(kzgx::gen_srs_g2_comb(ctx->c.curve, (const uint32_t*)d_tau, start, n, g.g2_comb, ctx->d_srs2_canon,
+                                 ctx->c.stream));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
   ctx->n_srs2 = n;
-  return KZGX_OK;
+  return setup_finish(ctx);
 }
 
 int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
@@ -876,7 +925,7 @@ int kzgx_load_srs_g2(kzgx_ctx* ctx, const uint64_t* xy, size_t n) {
   KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_srs2_canon, xy, bytes, hipMemcpyHostToDevice, ctx->c.stream));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
   ctx->n_srs2 = n;
-  return KZGX_OK;
+  return setup_finish(ctx);
 }
 
 int kzgx_get_srs_g2(kzgx_ctx* ctx, uint64_t* xy, size_t n) {
@@ -1021,7 +1070,9 @@ int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const 
   if (count <= ctx->vw_max) {
     if (!ctx->vw_ready) {
       KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
-      KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, ctx->d_vw, st));
+      kzgx::GenTables g;
+      KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, st, &g));
+      KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, g.g1_comb, ctx->d_vw, st));
       KZGX_TRY_HIP(hipStreamSynchronize(st));  // one-time; later calls may come on other streams
       ctx->vw_ready = true;
     }
@@ -1075,6 +1126,41 @@ int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const in
 }
 
 }  // extern "C"
+
+namespace {
+// Once both SRS halves are present (the end of trusted_setup(int) or of a
+// setup-file load): the verify tables (kzgx_verify_proof's [y]G table and the
+// line tables of G2[0], G2[1]) and the call workspaces are made here, so the
+// first commit / proof / verify on a new setup pays no allocation or table
+// build (the reference's benchmark times each first call,
+// benchmark/benchmark.cpp:40-66).  KZGX_LAZY_SETUP=1 leaves them to first use.
+int setup_finish(kzgx_ctx* ctx) {
+  static const bool lazy = std::getenv("KZGX_LAZY_SETUP") && std::getenv("KZGX_LAZY_SETUP")[0] == '1';
+  if (lazy || ctx->c.n_srs == 0 || ctx->n_srs2 < 2) return KZGX_OK;
+  hipStream_t st = ctx->c.stream;
+  kzgx::GenTables g;
+  KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, st, &g));
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
+  KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, g.g1_comb, ctx->d_vw, st));
+  // staging of the host-pointer calls, sized for degree-4096 single calls
+  KZGX_TRY(pin_stage(ctx, (size_t)1 << 20));
+  void* d;
+  for (int s = 0; s < 4; s++) KZGX_TRY(stage(ctx, s, (size_t)256 << 10, &d));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  ctx->vw_ready = true;
+  // the single-call workspaces (quotient, latency partials, arrival
+  // counters, Pippenger buffers): one zero proof at the largest default
+  // degree and one at degree 128 size them
+  const size_t nmax = std::min<size_t>(ctx->c.n_srs, 4097);
+  std::vector<uint64_t> zc(4 * nmax, 0), zz(4, 0), xy(2 * point_words(ctx), 0), y(4, 0);
+  int inf = 0;
+  for (size_t n : {nmax, std::min<size_t>(nmax, 129)}) {
+    KZGX_TRY(kzgx_prove_single_batch(ctx, zc.data(), n, 0, zz.data(), 1, xy.data(), &inf, y.data()));
+    KZGX_TRY(kzgx_msm_g1(ctx, zc.data(), n, xy.data(), &inf));
+  }
+  return KZGX_OK;
+}
+}  // namespace
 
 // Debug only (not part of include/kzg_gpu.h): copy a Pippenger workspace
 // buffer of the context's default stream to the host, after a device sync.

@@ -145,6 +145,11 @@ struct Ctx {
   uint32_t* d_table_small = nullptr;
   size_t table_small_bytes = 0;
   size_t n_small = 0;
+  // wide-window table of the large single MSMs (msm.hip, msm_big):
+  // [W_big][n_srs] at c_big bits, built with an SRS of >= 2^16 points
+  uint32_t* d_table_big = nullptr;
+  size_t table_big_bytes = 0;
+  int c_big = 0;  // 0: none / stale
   size_t small_batch = KZGX_SMALL_BATCH;  // largest batch that uses it (0: never)
   uint8_t* d_inf = nullptr;  // [n_srs]
   size_t inf_bytes = 0;
@@ -298,7 +303,10 @@ int verify_single_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_c
                         const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_ok, hipStream_t st);
 // wave-per-opening verify (pairing.hip): setup-derived tables, then the batch
 size_t verify_wave_bytes(int curve);
-int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st);
+// g1_comb: the generator's comb (kzgx_setup.hpp GenTables), copied into the
+// buffer when G1[0] is the generator; null: computed from G1[0]
+int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, const uint32_t* g1_comb,
+                        uint32_t* d_buf, hipStream_t st);
 int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_commit_inf, const uint32_t* d_proofs,
                       const uint32_t* d_proof_inf, const uint32_t* d_z, const uint32_t* d_y, size_t count,
                       const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st);

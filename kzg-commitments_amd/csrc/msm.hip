@@ -28,6 +28,7 @@
 #include "curve.hpp"
 #include "msm_merge.hpp"
 #include "kzgx_internal.hpp"
+#include "kzgx_setup.hpp"
 
 namespace kzgx {
 
@@ -637,6 +638,145 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
 }
 
 // --------------------------------------------------------------------------
+// large single MSMs (n >= 2^16): wide windows, global counting sort
+// --------------------------------------------------------------------------
+// One MSM of n points at c = 14..16 (2^13..2^15 buckets) instead of n / 4096
+// chunked c = 12 MSMs: n W additions (W = 17 at c = 16 against 22 at c = 12)
+// and ONE bucket reduction instead of one per chunk.  The wide window's
+// table T_big[w][i] = 2^(c w) P_i is built with the SRS (srs_upload).  The
+// sort is a two-pass counting sort over blocks of `per` scalars: each block
+// keeps its whole bucket histogram in LDS (2^(c-1) counters, up to 128 KB of
+// gfx950's 160 KB), a scan turns the block histograms into per-(block,
+// bucket) write bases, and the scatter ranks with LDS atomics that return
+// global positions directly.  Accumulation and segment merges are the
+// batched path's kernels; the bucket reduction runs in latency.hip.
+constexpr uint32_t BIG_TPB = 1024;  // threads of a count / scatter block
+
+template <int CB>
+__global__ __launch_bounds__(BIG_TPB) void k_big_count(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                       const uint8_t* __restrict__ inf, uint32_t per,
+                                                       uint32_t* __restrict__ counts) {
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  __shared__ uint32_t hist[NB];
+  for (uint32_t k = threadIdx.x; k < NB; k += BIG_TPB) hist[k] = 0;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+#pragma unroll 1
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += BIG_TPB) {
+    if (inf[i]) continue;
+    uint32_t s[8];
+    load_scalar(scalars + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int d = digit_at<CB>(s, w, carry);
+      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = counts + (size_t)blockIdx.x * NB;
+  for (uint32_t k = threadIdx.x; k < NB; k += BIG_TPB) out[k] = hist[k];
+}
+
+// bucket totals over the blocks (thread per bucket, coalesced over k)
+template <int CB>
+__global__ __launch_bounds__(256) void k_big_tot(const uint32_t* __restrict__ counts, uint32_t nblk,
+                                                 uint32_t* __restrict__ tot) {
+  constexpr uint32_t NB = Win<CB>::NB;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= NB) return;
+  uint32_t s = 0;
+  for (uint32_t b = 0; b < nblk; b++) s += counts[(size_t)b * NB + k];
+  tot[k] = s;
+}
+
+// exclusive scan of the NB totals -> offsets[0..NB] (one workgroup)
+template <int CB>
+__global__ __launch_bounds__(1024) void k_big_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ offsets) {
+  constexpr uint32_t NB = Win<CB>::NB;
+  constexpr uint32_t PER = NB / 1024;
+  static_assert(PER >= 1 && NB % 1024 == 0, "k_big_scan: c >= 11");
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t v[PER], local = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < PER; j++) {
+    v[j] = tot[t * PER + j];
+    local += v[j];
+  }
+  uint32_t x = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int w = 0; w < 16; w++) {
+      const uint32_t c = wsum[w];
+      wsum[w] = run;
+      run += c;
+    }
+    offsets[NB] = run;
+  }
+  __syncthreads();
+  uint32_t excl = x - local + wsum[wv];
+#pragma unroll
+  for (uint32_t j = 0; j < PER; j++) {
+    offsets[t * PER + j] = excl;
+    excl += v[j];
+  }
+}
+
+// write base of every (block, bucket): offsets[k] + the earlier blocks' counts
+template <int CB>
+__global__ __launch_bounds__(256) void k_big_bases(const uint32_t* __restrict__ counts, uint32_t nblk,
+                                                   const uint32_t* __restrict__ offsets, uint32_t* __restrict__ bbase) {
+  constexpr uint32_t NB = Win<CB>::NB;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= NB) return;
+  uint32_t base = offsets[k];
+  for (uint32_t b = 0; b < nblk; b++) {
+    bbase[(size_t)b * NB + k] = base;
+    base += counts[(size_t)b * NB + k];
+  }
+}
+
+// (table index | sign) entries into bucket order: LDS cursors start at the
+// block's write bases, so an LDS atomic returns the entry's global position
+template <int CB>
+__global__ __launch_bounds__(BIG_TPB) void k_big_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                         const uint8_t* __restrict__ inf, uint32_t per,
+                                                         const uint32_t* __restrict__ bbase,
+                                                         uint32_t* __restrict__ entries, uint32_t n_rows) {
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  __shared__ uint32_t cur[NB];
+  const uint32_t* bb = bbase + (size_t)blockIdx.x * NB;
+  for (uint32_t k = threadIdx.x; k < NB; k += BIG_TPB) cur[k] = bb[k];
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+#pragma unroll 1
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += BIG_TPB) {
+    if (inf[i]) continue;
+    uint32_t s[8];
+    load_scalar(scalars + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int d = digit_at<CB>(s, w, carry);
+      if (d != 0) {
+        const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+        entries[pos] = ((uint32_t)w * n_rows + i) | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------
 // Small batches (a single create_commit / create_proof, the reference's own
@@ -656,6 +796,21 @@ constexpr size_t SMALL_MAX_POINTS = 65536;
 #ifndef KZGX_SMALL_BATCH_J
 #define KZGX_SMALL_BATCH_J 16
 #endif
+
+// large single MSMs take the wide-window path from this many points
+// (KZGX_BIG_MIN; 0 turns the path off: chunked c = 12 batches as in round 4)
+static size_t big_min_points() {
+  static const size_t v = std::getenv("KZGX_BIG_MIN") ? std::strtoull(std::getenv("KZGX_BIG_MIN"), nullptr, 10)
+                                                      : (size_t)1 << 16;
+  return v ? v : ~(size_t)0;
+}
+// its window for an SRS of n points: fewer additions per point (n W) against
+// a longer bucket reduction (2^(c-1) buckets); KZGX_BIG_WINDOW pins it
+static int big_window_bits(size_t n) {
+  static const int pin = std::getenv("KZGX_BIG_WINDOW") ? std::atoi(std::getenv("KZGX_BIG_WINDOW")) : 0;
+  if (pin >= 14 && pin <= 16) return pin;
+  return n >= ((size_t)1 << 18) ? 16 : n >= ((size_t)1 << 17) ? 15 : 14;
+}
 
 template <class C>
 int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
@@ -680,6 +835,18 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
                        KZGX_SMALL_WINDOW_BITS);
     KZGX_TRY_HIP(hipGetLastError());
     ctx->n_small = ns;
+  }
+  // the wide-window table of the large single MSMs (window 0 = the
+  // Montgomery SRS, window 0 of the main table)
+  ctx->c_big = 0;
+  if (n >= big_min_points()) {
+    const int cb = big_window_bits(n);
+    const int WB = (257 + cb - 1) / cb;
+    KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_big, (size_t)WB * n * pw, &ctx->table_big_bytes));
+    KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_big, ctx->d_table, n * pw, hipMemcpyDeviceToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_table_build<C>, grd, blk, 0, ctx->stream, ctx->d_table_big, ctx->d_inf, (uint32_t)n, WB, cb);
+    KZGX_TRY_HIP(hipGetLastError());
+    ctx->c_big = cb;
   }
   ctx->n_srs = n;
   return fixed_build(ctx, d_canon, n);
@@ -857,6 +1024,83 @@ static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uin
   return KZGX_OK;
 }
 
+template <class C, int CB>
+static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                        hipStream_t st) {
+  constexpr int W = Win<CB>::W;
+  constexpr uint32_t NB = Win<CB>::NB;
+  const size_t emax = (size_t)n * W;
+  // count / scatter blocks of `per` scalars: ~128 blocks (their histograms,
+  // NB words each, are the scan's input)
+  uint32_t per = 2048;
+  while ((n + per - 1) / per > 128) per <<= 1;
+  const size_t nblk = (n + per - 1) / per;
+  uint32_t K = ctx->seg_k;
+  while (K > 8 && emax / K < 131072) K >>= 1;
+  const size_t smax = (emax + K - 1) / K;
+  const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
+  const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+  if (nblk > 65535 || nwg > 65535 || smax / 256 + 1 > 65535) return KZGX_ERR_ARG;
+  WsLease wsp = ctx->ws_for(st);
+  if (!wsp) return KZGX_ERR_ARG;
+  MsmWs& ws = *wsp;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, nblk * NB * 4, &ws.counts_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, (nblk + 1) * NB * 4, &ws.cursors_b));  // bases | totals
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, (NB + 1) * 4, &ws.offsets_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.entries, emax * 4, &ws.entries_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, NB * XB, &ws.bsum_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, smax * XB, &ws.heads_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, smax * XB, &ws.tails_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, smax * 4, &ws.tailk_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.sstate, smax, &ws.sstate_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.gpart, nwg * 2 * XB, &ws.gpart_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.gmeta, nwg * 2 * 4, &ws.gmeta_b));
+  KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, big_reduce_rt_bytes(ctx->curve, NB), &ws.rt_b));
+  uint32_t* tot = ws.cursors + nblk * NB;
+  uint32_t* ghead = ws.gpart;
+  uint32_t* gtail = ws.gpart + nwg * xyzz_words<C>();
+  uint32_t* gtailk = ws.gmeta;
+  uint32_t* gflag = ws.gmeta + nwg;
+  {
+    ProfScope p(ctx, st, "msm_sort");
+    hipLaunchKernelGGL(k_big_count<CB>, dim3((unsigned)nblk), dim3(BIG_TPB), 0, st, d_scalars, (uint32_t)n, ctx->d_inf,
+                       per, ws.counts);
+    hipLaunchKernelGGL(k_big_tot<CB>, dim3((NB + 255) / 256), dim3(256), 0, st, ws.counts, (uint32_t)nblk, tot);
+    hipLaunchKernelGGL(k_big_scan<CB>, dim3(1), dim3(1024), 0, st, tot, ws.offsets);
+    hipLaunchKernelGGL(k_big_bases<CB>, dim3((NB + 255) / 256), dim3(256), 0, st, ws.counts, (uint32_t)nblk,
+                       ws.offsets, ws.cursors);
+    hipLaunchKernelGGL(k_big_scatter<CB>, dim3((unsigned)nblk), dim3(BIG_TPB), 0, st, d_scalars, (uint32_t)n,
+                       ctx->d_inf, per, ws.cursors, ws.entries, (uint32_t)ctx->n_srs);
+  }
+  {
+    ProfScope p(ctx, st, "msm_accum");
+    hipLaunchKernelGGL(k_msm_accum<C>, dim3((unsigned)((smax + 255) / 256), 1), dim3(256), 0, st, ws.entries, emax,
+                       ws.offsets, NB, ctx->d_table_big, K, (uint32_t)smax, ws.bsum, ws.heads, ws.tails, ws.tailk,
+                       ws.sstate);
+  }
+  {
+    ProfScope p(ctx, st, "msm_reduce");
+    hipLaunchKernelGGL(k_msm_merge<C>, dim3((unsigned)nwg, 1), dim3(ACC_WG), 0, st, ws.heads, ws.tails, ws.tailk,
+                       ws.sstate, (uint32_t)smax, NB, (uint32_t)nwg, ws.bsum, ghead, gtail, gtailk, gflag);
+    hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg + 63) / 64), 1), dim3(64), 0, st, NB, (uint32_t)nwg,
+                       ghead, gtail, gtailk, gflag, ws.bsum);
+    KZGX_TRY_HIP(hipGetLastError());
+    KZGX_TRY(big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st));
+  }
+  return KZGX_OK;
+}
+
+template <class C>
+static int msm_big(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                   hipStream_t st) {
+  switch (ctx->c_big) {
+    case 14: return msm_big_impl<C, 14>(ctx, d_scalars, n, d_out, d_out_inf, st);
+    case 15: return msm_big_impl<C, 15>(ctx, d_scalars, n, d_out, d_out_inf, st);
+    case 16: return msm_big_impl<C, 16>(ctx, d_scalars, n, d_out, d_out_inf, st);
+    default: return KZGX_ERR_INTERNAL;
+  }
+}
+
 int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
   if (ctx->curve == KZGX_CURVE_BN254)
     hipLaunchKernelGGL(k_xyzz_sum<BN254G1>, dim3(1), dim3(256), 256 * xyzz_words<BN254G1>() * 4, st, d_parts,
@@ -890,6 +1134,11 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
 #ifndef KZGX_CHUNK_MIN
 #define KZGX_CHUNK_MIN (32 * MSM_CHUNK)
 #endif
+  // one large MSM: the wide-window path (its table exists for SRSs of
+  // >= big_min_points() points)
+  if (batch == 1 && ctx->c_big && n >= big_min_points())
+    return bn ? msm_big<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
+              : msm_big<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
   if (batch == 1 && n >= KZGX_CHUNK_MIN)
     return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
               : msm_single_chunked<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
@@ -897,4 +1146,14 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
             : msm_batch_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr);
 }
 
+}  // namespace kzgx
+
+namespace kzgx {
+// device bring-up (kzgx_setup.hpp): one launch loads this code object
+__global__ void k_warm_msm() {}
+int warm_msm(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_msm, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
 }  // namespace kzgx

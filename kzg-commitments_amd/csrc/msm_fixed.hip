@@ -32,6 +32,7 @@
 #include "curve.hpp"
 #include "fixed_accum.hpp"
 #include "kzgx_internal.hpp"
+#include "kzgx_setup.hpp"
 
 namespace kzgx {
 
@@ -596,22 +597,30 @@ static int fixed_build_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, s
   hipStream_t st = ctx->stream;
   hipLaunchKernelGGL(k_fixed_bases<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_canon, (uint32_t)n, W, c,
                      d_bases, d_inf);
-  const uint32_t J = (uint32_t)(H < FIXED_J ? H : FIXED_J);
-  const uint64_t tasks = (uint64_t)W * n * (H / J);
   ft.point_major = fixed_point_major(c, ft.layout_req);
   const TabStrides ts = fixed_strides<C>(ft.point_major, W, n, H);
-  // bounded launches of <= 2^22 threads each, synchronised per slice so one
-  // setup never queues seconds of work behind a single dispatch
-  const uint64_t slice = 1ull << 22;
-  for (uint64_t s0 = 0; s0 < tasks; s0 += slice) {
-    const uint64_t cnt = tasks - s0 < slice ? tasks - s0 : slice;
-    {
-      ProfScope p(ctx, st, "fixed_build");
-      hipLaunchKernelGGL(k_fixed_multiples<C>, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, d_bases, d_inf,
-                         (uint32_t)n, W, (uint32_t)H, J, s0, cnt, ts, ft.d);
+  // KZGX_TABLE_BUILD_SERIAL=1: the round-4 builder (one inversion per entry),
+  // for A/B runs of the batch-affine one (setup.hip)
+  static const bool serial = std::getenv("KZGX_TABLE_BUILD_SERIAL") && std::getenv("KZGX_TABLE_BUILD_SERIAL")[0] == '1';
+  if (!serial) {
+    ProfScope p(ctx, st, "fixed_build");
+    KZGX_TRY(fixed_multiples_batch(ctx->curve, d_bases, d_inf, (uint32_t)n, W, (uint32_t)H, ts.is, ts.ws, ft.d, st));
+  } else {
+    const uint32_t J = (uint32_t)(H < FIXED_J ? H : FIXED_J);
+    const uint64_t tasks = (uint64_t)W * n * (H / J);
+    // bounded launches of <= 2^22 threads each, synchronised per slice so one
+    // setup never queues seconds of work behind a single dispatch
+    const uint64_t slice = 1ull << 22;
+    for (uint64_t s0 = 0; s0 < tasks; s0 += slice) {
+      const uint64_t cnt = tasks - s0 < slice ? tasks - s0 : slice;
+      {
+        ProfScope p(ctx, st, "fixed_build");
+        hipLaunchKernelGGL(k_fixed_multiples<C>, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, d_bases, d_inf,
+                           (uint32_t)n, W, (uint32_t)H, J, s0, cnt, ts, ft.d);
+      }
+      KZGX_TRY_HIP(hipGetLastError());
+      KZGX_TRY_HIP(hipStreamSynchronize(st));
     }
-    KZGX_TRY_HIP(hipGetLastError());
-    KZGX_TRY_HIP(hipStreamSynchronize(st));
   }
   // whether any SRS point of the prefix is infinite: when none is (every SRS
   // but a degenerate tau = 0 one), the accumulation kernels get no flag array
@@ -666,7 +675,14 @@ static int fixed_build_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) 
 
 int fixed_build(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
   KZGX_TRY(fixed_build_table(ctx, ctx->fixed, d_canon, n_srs));
-  return fixed_build_default(ctx, d_canon, n_srs);
+  // the default table is an acceleration cache: if it cannot be built (any
+  // status) the SRS stays loaded and the MSMs take Pippenger
+  if (fixed_build_default(ctx, d_canon, n_srs) != KZGX_OK) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(ctx->stream);
+    fixed_free_table(ctx->fixed_def);
+  }
+  return KZGX_OK;
 }
 
 int fixed_rebuild_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
@@ -1149,4 +1165,14 @@ int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res) {
                                         : debug_latency_impl<BLS12381G1>(ctx, op, iters, res);
 }
 
+}  // namespace kzgx
+
+namespace kzgx {
+// device bring-up (kzgx_setup.hpp): one launch loads this code object
+__global__ void k_warm_msm_fixed() {}
+int warm_msm_fixed(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_msm_fixed, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
 }  // namespace kzgx

@@ -27,6 +27,7 @@
 
 #include "field.hpp"
 #include "kzgx_internal.hpp"
+#include "kzgx_setup.hpp"
 
 namespace kzgx {
 
@@ -759,4 +760,14 @@ int prove_range_poly(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_
                                         : prove_range_poly_impl<BLS12381Fr>(ctx, d_P, n, d_x, len, d_q, nq, st);
 }
 
+}  // namespace kzgx
+
+namespace kzgx {
+// device bring-up (kzgx_setup.hpp): one launch loads this code object
+__global__ void k_warm_poly() {}
+int warm_poly(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_poly, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
 }  // namespace kzgx

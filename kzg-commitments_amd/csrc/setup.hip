@@ -1,0 +1,385 @@
+// Setup-time kernels for gfx950: the per-process generator comb tables, the
+// comb SRS generation (G1 and G2) and the batch-affine builder of the
+// fixed-base tables.  Everything here runs inside trusted_setup(int) /
+// kzg::init (reference src/trusted_setup.cpp:21-135), never on the
+// commit / prove path.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "fixed_accum.hpp"
+#include "kzgx_setup.hpp"
+#include "pairing_common.hpp"
+
+namespace kzgx {
+
+__global__ void k_warm_setup() {}
+int warm_setup(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_setup, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+// ---- generator comb tables -------------------------------------------------
+// entry t = (w, d - 1): d 2^(8 w) G, by double-and-add from the top set bit
+template <class C>
+__global__ __launch_bounds__(64) void k_g1_comb(uint32_t* __restrict__ tab) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)GEN_COMB_ENTRIES) return;
+  using F = typename C::Fp29;
+  const uint32_t w = t / 255, d = t % 255 + 1;
+  Affine<C> g;
+  g.x = f29_const<F>(C::GX29);
+  g.y = f29_const<F>(C::GY29);
+  Xyzz<C> acc = xyzz_from_affine<C>(g);
+  for (int b = 30 - __builtin_clz(d); b >= 0; b--) {
+    acc = xyzz_dbl<C>(acc);
+    if ((d >> b) & 1u) acc = xyzz_add_affine<C>(acc, g);
+  }
+  for (uint32_t s = 0; s < 8 * w; s++) acc = xyzz_dbl<C>(acc);
+  Affine<C> a;
+  if (!xyzz_to_affine<C>(acc, a)) a.x = a.y = f29_zero<F>();  // never: d 2^(8w) < r
+  affine_store<C>(tab + (size_t)t * affine_words<C>(), a);
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void k_g2_comb(G2A<C>* __restrict__ tab) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)GEN_COMB_ENTRIES) return;
+  using P = typename PairOf<C>::T;
+  const uint32_t w = t / 255, d = t % 255 + 1;
+  G2A<C> q;
+  q.x = f2_const<C>(P::G2X);
+  q.y = f2_const<C>(P::G2Y);
+  G2J<C> acc = g2_from_affine<C>(q);
+  for (int b = 30 - __builtin_clz(d); b >= 0; b--) {
+    acc = g2_dbl<C>(acc);
+    if ((d >> b) & 1u) acc = g2_add_mixed<C>(acc, q);
+  }
+  for (uint32_t s = 0; s < 8 * w; s++) acc = g2_dbl<C>(acc);
+  G2A<C> a;
+  if (!g2_to_affine<C>(acc, a)) a.x = a.y = f2_zero<C>();  // never: the generator has order r
+  tab[t] = a;
+}
+
+namespace {
+std::mutex g_gen_mu;
+std::map<std::pair<int, int>, GenTables> g_gen;  // (device, curve) -> tables, kept until exit
+
+template <class C>
+int gen_tables_build(GenTables& g, hipStream_t st) {
+  const unsigned blocks = (GEN_COMB_ENTRIES + 63) / 64;
+  KZGX_TRY_HIP(hipMalloc((void**)&g.g1_comb, (size_t)GEN_COMB_ENTRIES * affine_words<C>() * 4));
+  KZGX_TRY_HIP(hipMalloc((void**)&g.g2_comb, (size_t)GEN_COMB_ENTRIES * sizeof(G2A<C>)));
+  hipLaunchKernelGGL(k_g1_comb<C>, dim3(blocks), dim3(64), 0, st, g.g1_comb);
+  hipLaunchKernelGGL(k_g2_comb<C>, dim3(blocks), dim3(64), 0, st, (G2A<C>*)g.g2_comb);
+  KZGX_TRY_HIP(hipGetLastError());
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  return KZGX_OK;
+}
+}  // namespace
+
+int gen_tables_get(int curve, int device, hipStream_t st, GenTables* out) {
+  std::lock_guard<std::mutex> lk(g_gen_mu);
+  const auto key = std::make_pair(device, curve);
+  auto it = g_gen.find(key);
+  if (it == g_gen.end()) {
+    GenTables g;
+    const int rc = curve == KZGX_CURVE_BN254 ? gen_tables_build<BN254G1>(g, st) : gen_tables_build<BLS12381G1>(g, st);
+    if (rc != KZGX_OK) {
+      if (g.g1_comb) (void)hipFree(g.g1_comb);
+      if (g.g2_comb) (void)hipFree(g.g2_comb);
+      return rc;
+    }
+    it = g_gen.emplace(key, g).first;
+  }
+  *out = it->second;
+  return KZGX_OK;
+}
+
+// ---- comb SRS generation -----------------------------------------------------
+// e = tau^ex mod r, canonical words (square-and-multiply from the top set bit)
+template <class C>
+KZGX_DEV Fe<typename C::Fr> srs_power(const uint32_t* tau_canon, uint64_t ex) {
+  using FR = typename C::Fr;
+  const Fe<FR> tm = fe_to_mont<FR>(fe_load<FR>(tau_canon));
+  Fe<FR> e = fe_one<FR>();
+  for (int b = 63 - __builtin_clzll(ex | 1ull); b >= 0; b--) {
+    e = fe_sqr<FR>(e);
+    if ((ex >> b) & 1ull) e = fe_mul<FR>(e, tm);
+  }
+  return fe_from_mont<FR>(e);
+}
+
+// two points per wave: lanes 32 g + w (w < 32) hold window w's comb entry of
+// point 2 blockIdx.x + g; a shuffle tree (xor 16 .. 1) sums the 32 entries
+template <class C>
+__global__ __launch_bounds__(64) void k_gen_srs_comb(const uint32_t* __restrict__ tau_canon, uint64_t start, uint32_t n,
+                                                     const uint32_t* __restrict__ comb, uint32_t* __restrict__ out) {
+  constexpr int L = C::Fp29::L;
+  const uint32_t lane = threadIdx.x, w = lane & 31;
+  const uint32_t i = blockIdx.x * 2 + (lane >> 5);
+  const bool live = i < n;  // dead lanes still take part in the shuffles
+  Xyzz<C> p = xyzz_inf<C>();
+  if (live) {
+    const auto e = srs_power<C>(tau_canon, start + i);
+    const uint32_t d = (e.v[w >> 2] >> (8 * (w & 3))) & 255u;
+    if (d) p = xyzz_from_affine<C>(affine_load<C>(comb + ((size_t)w * 255 + d - 1) * affine_words<C>()));
+  }
+  for (int off = 16; off >= 1; off >>= 1) {
+    Xyzz<C> o;
+#pragma unroll
+    for (int k = 0; k < L; k++) {
+      o.X.v[k] = __shfl_xor(p.X.v[k], off, 32);
+      o.Y.v[k] = __shfl_xor(p.Y.v[k], off, 32);
+      o.ZZ.v[k] = __shfl_xor(p.ZZ.v[k], off, 32);
+      o.ZZZ.v[k] = __shfl_xor(p.ZZZ.v[k], off, 32);
+    }
+    p = xyzz_add<C>(p, o);
+  }
+  if (live && w == 0) {
+    Affine<C> a;
+    const bool fin = xyzz_to_affine<C>(p, a);
+    affine_to_canonical<C>(out + (size_t)i * 2 * C::Fp::N, a, fin);
+  }
+}
+
+template <class C>
+KZGX_DEV void g2j_shfl_xor(G2J<C>& o, const G2J<C>& p, int off) {
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++) {
+    o.X.a.v[k] = __shfl_xor(p.X.a.v[k], off, 32);
+    o.X.b.v[k] = __shfl_xor(p.X.b.v[k], off, 32);
+    o.Y.a.v[k] = __shfl_xor(p.Y.a.v[k], off, 32);
+    o.Y.b.v[k] = __shfl_xor(p.Y.b.v[k], off, 32);
+    o.Z.a.v[k] = __shfl_xor(p.Z.a.v[k], off, 32);
+    o.Z.b.v[k] = __shfl_xor(p.Z.b.v[k], off, 32);
+  }
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void k_gen_srs_g2_comb(const uint32_t* __restrict__ tau_canon, uint64_t start,
+                                                        uint32_t n, const G2A<C>* __restrict__ comb,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x, w = lane & 31;
+  const uint32_t i = blockIdx.x * 2 + (lane >> 5);
+  const bool live = i < n;
+  G2J<C> p = g2_inf<C>();
+  if (live) {
+    const auto e = srs_power<C>(tau_canon, start + i);
+    const uint32_t d = (e.v[w >> 2] >> (8 * (w & 3))) & 255u;
+    if (d) p = g2_from_affine<C>(comb[(size_t)w * 255 + d - 1]);
+  }
+  for (int off = 16; off >= 1; off >>= 1) {
+    G2J<C> o;
+    g2j_shfl_xor<C>(o, p, off);
+    p = g2_add<C>(p, o);
+  }
+  if (live && w == 0) {
+    G2A<C> a;
+    const bool fin = g2_to_affine<C>(p, a);
+    g2_to_canon<C>(a, fin, out + (size_t)i * 4 * C::Fp::N);
+  }
+}
+
+int gen_srs_g1_comb(int curve, const uint32_t* d_tau, size_t start, size_t n, const uint32_t* g1_comb,
+                    uint32_t* d_out, hipStream_t st) {
+  const dim3 grd((unsigned)((n + 1) / 2)), blk(64);
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_gen_srs_comb<BN254G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, g1_comb, d_out);
+  else
+    hipLaunchKernelGGL(k_gen_srs_comb<BLS12381G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n, g1_comb,
+                       d_out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int gen_srs_g2_comb(int curve, const uint32_t* d_tau, size_t start, size_t n, const uint32_t* g2_comb,
+                    uint32_t* d_out, hipStream_t st) {
+  const dim3 grd((unsigned)((n + 1) / 2)), blk(64);
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_gen_srs_g2_comb<BN254G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n,
+                       (const G2A<BN254G1>*)g2_comb, d_out);
+  else
+    hipLaunchKernelGGL(k_gen_srs_g2_comb<BLS12381G1>, grd, blk, 0, st, d_tau, (uint64_t)start, (uint32_t)n,
+                       (const G2A<BLS12381G1>*)g2_comb, d_out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+// ---- verify's [y]G table -----------------------------------------------------
+// entry t of the comb of G1[0]: copied from the generator's comb when G1[0]
+// is the generator (every generated setup, every reference setup file),
+// else d 2^(8w) G1[0] by double-and-add
+template <class C>
+__global__ __launch_bounds__(64) void k_vtab_prepare(const uint32_t* __restrict__ g1_0, const uint32_t* __restrict__ comb,
+                                                     uint32_t* __restrict__ tab) {
+  using F = typename C::Fp29;
+  constexpr int AW = affine_words<C>();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)GEN_COMB_ENTRIES) return;
+  Affine<C> g;
+  const bool fin = affine_from_canonical<C>(g1_0, g);
+  const F29<F> gx = f29_reduce<F>(g.x), gy = f29_reduce<F>(g.y);
+  bool gen = fin;
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++) gen = gen && gx.v[k] == C::GX29[k] && gy.v[k] == C::GY29[k];
+  if (gen) {
+    for (int k = 0; k < AW; k++) tab[(size_t)t * AW + k] = comb[(size_t)t * AW + k];
+    return;
+  }
+  const uint32_t w = t / 255, d = t % 255 + 1;
+  Affine<C> a;
+  a.x = a.y = f29_zero<F>();
+  if (fin) {
+    uint32_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e[w >> 2] = d << (8 * (w & 3));
+    if (!xyzz_to_affine<C>(g1_mul_words<C>(g, e), a)) a.x = a.y = f29_zero<F>();
+  }
+  affine_store<C>(tab + (size_t)t * AW, a);
+}
+
+int vtab_prepare(int curve, const uint32_t* d_g1_0, const uint32_t* g1_comb, uint32_t* d_vtab, hipStream_t st) {
+  const dim3 grd((GEN_COMB_ENTRIES + 63) / 64), blk(64);
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_vtab_prepare<BN254G1>, grd, blk, 0, st, d_g1_0, g1_comb, d_vtab);
+  else
+    hipLaunchKernelGGL(k_vtab_prepare<BLS12381G1>, grd, blk, 0, st, d_g1_0, g1_comb, d_vtab);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+// ---- fixed-base table: batch-affine odd multiples --------------------------------
+// Task g = ((w n + i) G + grp): entries j in [grp per, (grp + 1) per) of
+// M(w, i, j) = (2 j + 1) B, B = B[w][i].  Chain k < K = 16 holds the entries
+// j = grp per + K m + k; its first entry (2 j0 + 2 k + 1) B comes from a
+// double-and-add and per-entry conversions, then every step adds S = 2K B
+// to all K chains in affine form, their K inversions batched into one:
+//   d_k = S.x - x_k, prefix products, one inversion, back-substitution,
+//   lambda = (S.y - y_k) / d_k, x' = lambda^2 - x_k - S.x, y' = lambda (x_k - x') - y_k
+// 6K - 3 products + 1 inversion per K entries, against a mixed addition and
+// an inversion per entry for the single-chain builder.  The previous step's
+// entries are read back from the table (the thread's own writes, L2-hot).
+// None of the additions meets an exceptional case: (2 j + 1) B = +-2K B is
+// impossible for B of order r, 2 j + 1 < 2^17 odd and 2K = 32 even.
+template <class F>
+KZGX_DEV void f29_store_raw(uint32_t* p, const F29<F>& a) {
+#pragma unroll
+  for (int i = 0; i < F::L; i++) p[i] = a.v[i];
+}
+template <class F>
+KZGX_DEV F29<F> f29_load_raw(const uint32_t* p) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < F::L; i++) r.v[i] = p[i];
+  return r;
+}
+
+constexpr int FM_K = 16;
+constexpr uint32_t FM_PER = 1024;  // entries per thread (<= H)
+
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_multiples_batch(const uint32_t* __restrict__ bases,
+                                                              const uint8_t* __restrict__ inf, uint32_t n, uint32_t H,
+                                                              uint32_t per, uint64_t t0, uint64_t cnt, TabStrides ts,
+                                                              uint32_t* __restrict__ tab) {
+  using F = typename C::Fp29;
+  constexpr int PW = packed_words<C>();
+  constexpr int K = FM_K;
+  const uint64_t gl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gl >= cnt) return;
+  const uint32_t G = H / per;
+  const uint64_t g = t0 + gl;
+  const uint32_t grp = (uint32_t)(g % G);
+  const uint64_t wi = g / G;  // w n + i
+  const uint32_t i = (uint32_t)(wi % n), w = (uint32_t)(wi / n);
+  uint32_t* out = tab + (uint64_t)i * ts.is + (uint64_t)w * ts.ws + (uint64_t)grp * per * PW;
+  if (inf[i]) {  // never read: the MSMs skip infinite SRS points
+    for (uint32_t j = 0; j < per * PW; j++) out[j] = 0;
+    return;
+  }
+  const Affine<C> B = packed_load<C>(bases + wi * PW);
+  const Xyzz<C> b2 = xyzz_dbl_affine<C>(B);
+  // chain starts (2 j0 + 1 + 2 k) B, k < min(per, K)
+  const uint32_t k0 = 2 * grp * per + 1;
+  Xyzz<C> acc = xyzz_from_affine<C>(B);
+  for (int bit = 30 - __builtin_clz(k0); bit >= 0; bit--) {
+    acc = xyzz_dbl<C>(acc);
+    if ((k0 >> bit) & 1u) acc = xyzz_add_affine<C>(acc, B);
+  }
+  const uint32_t KK = per < (uint32_t)K ? per : (uint32_t)K;
+  for (uint32_t k = 0; k < KK; k++) {
+    if (k) acc = xyzz_add<C>(acc, b2);
+    Affine<C> a;
+    xyzz_to_affine<C>(acc, a);
+    packed_store<C>(out + (size_t)k * PW, a);
+  }
+  if (per <= (uint32_t)K) return;
+  Xyzz<C> s = b2;
+  static_assert(K == 16, "S = 2K B below");
+#pragma unroll
+  for (int t = 0; t < 4; t++) s = xyzz_dbl<C>(s);  // 32 B = 2 K B
+  Affine<C> S;
+  xyzz_to_affine<C>(s, S);
+  const uint32_t steps = per / K;
+  for (uint32_t m = 1; m < steps; m++) {
+    const uint32_t* prev = out + (size_t)(m - 1) * K * PW;
+    uint32_t* cur = out + (size_t)m * K * PW;
+    // prefix products d_0 ... d_k go into the step's own (still empty)
+    // table slots, so nothing but S is live across the inversion call
+    // (in registers, pre[] held the kernel at 1 wave per SIMD)
+    F29<F> pre;
+    static_for<0, K>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const Affine<C> a = packed_load<C>(prev + k * PW);
+      const F29<F> d = f29_sub<F>(S.x, a.x, F::P2);  // S.x + 2m - x in (m, 3m)
+      if constexpr (k == 0) pre = d;
+      else pre = f29_mul<F>(pre, d);
+      if constexpr (k + 1 < K) f29_store_raw<F>(cur + (size_t)k * PW, pre);
+    });
+    F29<F> inv = f29_inv_fast<F, C::Fp::N>(pre, C::Fp::P, C::Fp::PM2);
+    static_for<0, K>([&](auto kc) {
+      constexpr int k = K - 1 - decltype(kc)::value;
+      const Affine<C> a = packed_load<C>(prev + k * PW);
+      F29<F> ik = inv;
+      if constexpr (k > 0) {
+        ik = f29_mul<F>(inv, f29_load_raw<F>(cur + (size_t)(k - 1) * PW));
+        inv = f29_mul<F>(inv, f29_sub<F>(S.x, a.x, F::P2));
+      }
+      const F29<F> lam = f29_mul<F>(f29_sub<F>(S.y, a.y, F::P2), ik);             // (< 3m)(< 2m) -> < 2m
+      const F29<F> x3 = f29_sub<F>(f29_sqr<F>(lam), f29_add<F>(a.x, S.x), F::P4);  // < 6m
+      const F29<F> t = f29_mul<F>(lam, f29_sub<F>(a.x, x3, F::P8));                // (< 2m)(< 9m) -> < 2m
+      Affine<C> r;
+      r.x = f29_reduce<F>(x3);
+      r.y = f29_reduce<F>(f29_sub<F>(t, a.y, F::P2));  // < 4m
+      packed_store<C>(cur + (size_t)k * PW, r);  // slot k's prefix was consumed by step k + 1
+    });
+  }
+}
+
+int fixed_multiples_batch(int curve, const uint32_t* d_bases, const uint8_t* d_inf, uint32_t n, int W, uint32_t H,
+                          size_t is, size_t ws, uint32_t* d_tab, hipStream_t st) {
+  const uint32_t per = H < FM_PER ? H : FM_PER;
+  const uint64_t tasks = (uint64_t)W * n * (H / per);
+  const TabStrides ts{is, ws};
+  // bounded launches, synchronised per slice so one setup never queues
+  // seconds of work behind a single dispatch
+  const uint64_t slice = 1ull << 21;
+  for (uint64_t s0 = 0; s0 < tasks; s0 += slice) {
+    const uint64_t cnt = tasks - s0 < slice ? tasks - s0 : slice;
+    const dim3 grd((unsigned)((cnt + 63) / 64)), blk(64);
+    if (curve == KZGX_CURVE_BN254)
+      hipLaunchKernelGGL(k_fixed_multiples_batch<BN254G1>, grd, blk, 0, st, d_bases, d_inf, n, H, per, s0, cnt, ts,
+                         d_tab);
+    else
+      hipLaunchKernelGGL(k_fixed_multiples_batch<BLS12381G1>, grd, blk, 0, st, d_bases, d_inf, n, H, per, s0, cnt, ts,
+                         d_tab);
+    KZGX_TRY_HIP(hipGetLastError());
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+  }
+  return KZGX_OK;
+}
+
+}  // namespace kzgx

@@ -10,6 +10,7 @@
 
 #include "curve.hpp"
 #include "kzgx_internal.hpp"
+#include "kzgx_setup.hpp"
 
 namespace kzgx {
 
@@ -120,4 +121,14 @@ int g1_validate(Ctx* ctx, const uint32_t* d_xy, uint32_t* d_ok, hipStream_t st) 
   return KZGX_OK;
 }
 
+}  // namespace kzgx
+
+namespace kzgx {
+// device bring-up (kzgx_setup.hpp): one launch loads this code object
+__global__ void k_warm_srs() {}
+int warm_srs(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_srs, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
 }  // namespace kzgx

@@ -5,7 +5,12 @@
 // pairing.hip to keep each translation unit's compile time bounded.
 #include <hip/hip_runtime.h>
 
+// every Fp product in this translation unit (wave ops, tower, curve) takes
+// the latency-first form (field29.hpp f29_mul_lat): these kernels run as one
+// wave per pairing, where a product's dependency chain is the cost
+#define KZGX_FIELD_LATENCY
 #include "pairing_common.hpp"
+#include "kzgx_setup.hpp"
 
 namespace kzgx {
 
@@ -162,111 +167,70 @@ __global__ __launch_bounds__(64) void k_vtab(const uint32_t* __restrict__ g1_0, 
   affine_store<C>(tab + (size_t)t * V::AW, a);
 }
 
-// Lazy signed combination sum_j c_j p_j of values < 2m with normalized
-// limbs and small integer c_j: the positive and negative parts accumulate
-// limb-wise in 64 bits (one v_mad_u64_u32 per limb and sign), then one
-// carry pass each, one subtraction and a csub chain.  This replaces a
-// carried, reduced add per term (the bulk of a round's instructions).
-// Bounds: sum of positive c_j <= 16 and of negative |c_j| <= 16 -> the
-// difference + 32m lies in [0, 64m), reduced to < 2m.
+// Lazy signed combination sum_j c_j p_j of values with limbs < 2^31 and
+// small integer c_j: one signed 64-bit accumulator per limb (one
+// v_mad_i64_i32 per limb and term), then lin_fin reduces the value v
+// (|v| < 2^20 m) to [0, 2m) in one step: the quotient q = floor(v/m) is
+// estimated in double precision from the top three limb sums, and v - q m is
+// carry-normalized once.  The estimate's error (dropped limbs < 2^-20 m,
+// rounding < 2^-40) is far below the 2^-12 bias, so q is floor(v/m) or one
+// less: the result lies in (0, 2m).  This replaces a carry pass per sign, a
+// subtraction and a chain of conditional subtractions (~240 dependent
+// instructions on the lone wave) with ~40.
 template <class F>
 struct LinAcc {
-  uint64_t pos[F::L], neg[F::L];
+  int64_t v[F::L];
+};
+constexpr double lin_pow29(int k) {
+  double s = 1.0;
+  for (int i = 0; i < k; i++) s *= 536870912.0;
+  return s;
+}
+template <class F>
+constexpr double lin_modulus() {
+  double s = 0.0;
+  for (int i = F::L - 1; i >= 0; i--) s = s * 536870912.0 + (double)F::P[i];
+  return s;
+}
+template <class F>
+struct LinInvM {  // 2^(29 l) / m for the top three limbs
+  static constexpr double T0 = lin_pow29(F::L - 1) / lin_modulus<F>();
+  static constexpr double T1 = lin_pow29(F::L - 2) / lin_modulus<F>();
+  static constexpr double T2 = lin_pow29(F::L - 3) / lin_modulus<F>();
 };
 template <class F>
 KZGX_DEV void lin_init(LinAcc<F>& a) {
 #pragma unroll
-  for (int l = 0; l < F::L; l++) a.pos[l] = a.neg[l] = 0;
+  for (int l = 0; l < F::L; l++) a.v[l] = 0;
 }
 template <class F>
 KZGX_DEV void lin_add(LinAcc<F>& a, const uint32_t* p, int c) {
-  const uint32_t cp = c > 0 ? (uint32_t)c : 0u, cn = c < 0 ? (uint32_t)(-c) : 0u;
 #pragma unroll
-  for (int l = 0; l < F::L; l++) {
-    const uint32_t x = p[l];
-    a.pos[l] += (uint64_t)x * cp;
-    a.neg[l] += (uint64_t)x * cn;
-  }
+  for (int l = 0; l < F::L; l++) a.v[l] += (int64_t)(int32_t)p[l] * (int64_t)c;
 }
 template <class F>
 KZGX_DEV void lin_add(LinAcc<F>& a, const F29<F>& p, int c) {
   lin_add<F>(a, p.v, c);
 }
 template <class F>
-KZGX_DEV F29<F> lin_carry(const uint64_t (&v)[F::L]) {
+KZGX_DEV F29<F> lin_fin(const LinAcc<F>& a) {
+  constexpr int L = F::L;
+  const double x = (double)a.v[L - 1] * LinInvM<F>::T0 + (double)a.v[L - 2] * LinInvM<F>::T1 +
+                   (double)a.v[L - 3] * LinInvM<F>::T2;
+  const int64_t q = (int64_t)__builtin_floor(x - 0x1p-12);
   F29<F> r;
-  uint64_t c = 0;
+  int64_t c = 0;
 #pragma unroll
-  for (int l = 0; l < F::L; l++) {
-    const uint64_t t = v[l] + c;
-    r.v[l] = l + 1 < F::L ? ((uint32_t)t & M29) : (uint32_t)t;
-    c = t >> 29;
+  for (int l = 0; l < L; l++) {
+    const int64_t s = a.v[l] - q * (int64_t)F::P[l] + c;
+    if (l + 1 < L) {
+      r.v[l] = (uint32_t)s & M29;
+      c = s >> 29;  // arithmetic
+    } else {
+      r.v[l] = (uint32_t)s;
+    }
   }
   return r;
-}
-template <class F>
-KZGX_DEV F29<F> lin_fin(const LinAcc<F>& a) {
-  uint32_t k32[F::L];
-#pragma unroll
-  for (int l = 0; l < F::L; l++) k32[l] = 2u * F::P16[l];  // 32m, limbs < 2^30
-  F29<F> r = f29_sub<F>(lin_carry<F>(a.pos), lin_carry<F>(a.neg), k32);
-  r = f29_csub<F>(r, k32);
-  r = f29_csub<F>(r, F::P16);
-  r = f29_csub<F>(r, F::P8);
-  r = f29_csub<F>(r, F::P4);
-  return f29_csub<F>(r, F::P2);
-}
-
-// ---- Fp12 (w basis) in LDS, wave-cooperative; every op ends with a barrier
-// dst = a b (dst may alias a or b)
-template <class C>
-KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o) {
-  uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
-  const uint32_t *a = vw_smem + a_o, *b = vw_smem + b_o;
-  using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
-  const int lane = threadIdx.x;
-  if (lane < 36) {
-    const int i = lane / 6, j = lane % 6;
-    vw_st2<C>(prod + lane * E2, f2_mul<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(b + j * E2)));
-  }
-  __syncthreads();
-  if (lane < 12) {
-    // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij,  xi (t0 + t1 i) = (t0 - t1) + (t0 + t1) i
-    const int k = lane >> 1, im = lane & 1;
-    LinAcc<F> acc;
-    lin_init<F>(acc);
-    for (int i = 0; i < 6; i++) {
-      const int j = k - i;
-      if (j >= 0) lin_add<F>(acc, prod + (i * 6 + j) * E2 + im * L, 1);
-      const int j2 = k + 6 - i;
-      if (j2 < 6) {
-        const uint32_t* p = prod + (i * 6 + j2) * E2;
-        lin_add<F>(acc, p, 1);
-        lin_add<F>(acc, p + L, im ? 1 : -1);
-      }
-    }
-    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
-  }
-  __syncthreads();
-}
-
-// as lin_fin for positive parts up to 32 units (value < 64m + 32m)
-template <class F>
-KZGX_DEV F29<F> lin_fin_wide(const LinAcc<F>& a) {
-  uint32_t k32[F::L], k64[F::L];
-#pragma unroll
-  for (int l = 0; l < F::L; l++) {
-    k32[l] = 2u * F::P16[l];
-    k64[l] = 4u * F::P16[l];
-  }
-  F29<F> r = f29_sub<F>(lin_carry<F>(a.pos), lin_carry<F>(a.neg), k32);
-  r = f29_csub<F>(r, k64);
-  r = f29_csub<F>(r, k32);
-  r = f29_csub<F>(r, F::P16);
-  r = f29_csub<F>(r, F::P8);
-  r = f29_csub<F>(r, F::P4);
-  return f29_csub<F>(r, F::P2);
 }
 
 // Karatsuba parts of an Fp2 product x y: 0 = xa ya, 1 = xb yb,
@@ -296,6 +260,42 @@ KZGX_DEV void lin_add_f2(LinAcc<F>& acc, const uint32_t* q, int im, bool xi, int
   lin_add<F>(acc, q, d * c0);
   lin_add<F>(acc, q + L, d * c1);
   lin_add<F>(acc, q + 2 * L, d * c2);
+}
+
+// ---- Fp12 (w basis) in LDS, wave-cooperative; every op ends with a barrier
+// dst = a b (dst may alias a or b): the 36 Fp2 products a_i b_j as 108 Fp
+// (Karatsuba) parts, two independent products per lane (54 lanes), then lane
+// (k, im) < 12 folds the six products landing on w^k (xi for the wrapped
+// ones) lazily
+template <class C>
+KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o) {
+  uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
+  const uint32_t *a = vw_smem + a_o, *b = vw_smem + b_o;
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  const int lane = threadIdx.x;
+  if (lane < 54) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int t = lane + 54 * h, pr = t / 3;
+      vw_st<C>(prod + t * L, vw_part<C>(vw_ld2<C>(a + (pr / 6) * E2), vw_ld2<C>(b + (pr % 6) * E2), t % 3));
+    }
+  }
+  __syncthreads();
+  if (lane < 12) {
+    // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij
+    const int k = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      const bool wrap = i > k;
+      const int j = wrap ? k + 6 - i : k - i;
+      lin_add_f2<F>(acc, prod + (i * 6 + j) * 3 * L, im, wrap, 1);
+    }
+    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
 }
 
 // f = f l for a scaled line l = (l0, l1, l3) at positions (POS0, POS1, POS3):
@@ -375,14 +375,30 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
 // Granger-Scott squaring of a cyclotomic element (f12_cyclo_sqr) with one Fp
 // product per lane.  In the w basis the three Fp4 squarings pair (a_j, a_{j+3}),
 // j = 0, 1, 2: fp4_sqr(x, y) needs t = x y and u = (x + y)(x + xi y), each
-// an Fp2 Karatsuba product of 3 Fp products -> 18 lanes.  Then, with
-// c0_j = u - t - xi t and c1_j = 2 t:
+// an Fp2 Karatsuba product of 3 Fp products -> 18 lanes.  The operands are
+// formed lazily: limb-wise sums of the loaded coefficients (xi y and the
+// sums inside a Karatsuba part folded in), 2m added limb-wise under the one
+// negative term, then a single carry pass -- values < 10 m, products
+// < 80 m^2 < (R/m) m^2.  Then, with c0_j = u - t - xi t and c1_j = 2 t:
 //   a0' = 3 c0_0 - 2 a0   a2' = 3 c0_1 - 2 a2   a4' = 3 c0_2 - 2 a4
 //   a3' = 3 c1_0 + 2 a3   a5' = 3 c1_1 + 2 a5   a1' = 3 xi c1_2 + 2 a1
 // In parts p (of t) and q (of u):
 //   c0.re = q0 - q1 - 3 p0 + p1 + p2      c0.im = q2 - q0 - q1 + p0 + 3 p1 - 2 p2
 //   c1.re = 2 p0 - 2 p1                   c1.im = 2 p2 - 2 p0 - 2 p1
 //   (xi c1).re = 4 p0 - 2 p2              (xi c1).im = 2 p2 - 4 p1
+// folded in one lazy sum per output component (3 x the parts, +-2 a_k).
+template <class F>
+KZGX_DEV F29<F> vw_norm(const uint32_t (&o)[F::L]) {
+  F29<F> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    const uint32_t t = o[l] + c;
+    r.v[l] = l + 1 < F::L ? (t & M29) : t;
+    c = t >> 29;
+  }
+  return r;
+}
 template <class C>
 KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
@@ -391,14 +407,22 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   const uint32_t* a = vw_smem + a_o;
   const int lane = threadIdx.x;
   if (lane < 18) {
-    const int j = lane / 6, which = (lane / 3) & 1;
-    const Fp2<C> x = vw_ld2<C>(a + j * E2), y = vw_ld2<C>(a + (j + 3) * E2);
-    Fp2<C> X = x, Y = y;
-    if (which) {
-      X = f2_add<C>(x, y);
-      Y = f2_add<C>(x, f2_mul_xi<C>(y));
+    const int j = lane / 6, which = (lane / 3) & 1, part = lane % 3;
+    const uint32_t *xp = a + j * E2, *yp = a + (j + 3) * E2;
+    // part 0: (re, re), 1: (im, im), 2: (re + im, re + im) of
+    // t: (x, y);  u: (x + y, x + xi y), x + xi y = (xa + ya - yb, xb + ya + yb)
+    const uint32_t e0 = part != 1 ? ~0u : 0u, e1 = part != 0 ? ~0u : 0u, w = which ? ~0u : 0u;
+    const uint32_t y2 = part == 2 ? ~0u : 0u, yn = part == 0 ? ~0u : 0u, yp1 = part == 1 ? ~0u : 0u;
+    uint32_t o0[L], o1[L];
+#pragma unroll
+    for (int l = 0; l < L; l++) {
+      const uint32_t xa = xp[l], xb = xp[L + l], ya = yp[l], yb = yp[L + l];
+      const uint32_t sx = (xa & e0) + (xb & e1), sy = (ya & e0) + (yb & e1);
+      o0[l] = sx + (sy & w);
+      const uint32_t u1 = sx + ya + (ya & y2) + ((F::P2B[l] - yb) & yn) + (yb & yp1);
+      o1[l] = which ? u1 : sy;
     }
-    vw_st<C>(prod + lane * L, vw_part<C>(X, Y, lane % 3));
+    vw_st<C>(prod + lane * L, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
   }
   __syncthreads();
   if (lane < 12) {
@@ -424,15 +448,12 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     }
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add<F>(acc, q, cp0);
-    lin_add<F>(acc, q + L, cp1);
-    lin_add<F>(acc, q + 2 * L, cp2);
-    lin_add<F>(acc, q + 3 * L, cq0);
-    lin_add<F>(acc, q + 4 * L, cq1);
-    lin_add<F>(acc, q + 5 * L, cq2);
-    const F29<F> c = lin_fin<F>(acc);
-    lin_init<F>(acc);
-    lin_add<F>(acc, c, 3);
+    lin_add<F>(acc, q, 3 * cp0);
+    lin_add<F>(acc, q + L, 3 * cp1);
+    lin_add<F>(acc, q + 2 * L, 3 * cp2);
+    lin_add<F>(acc, q + 3 * L, 3 * cq0);
+    lin_add<F>(acc, q + 4 * L, 3 * cq1);
+    lin_add<F>(acc, q + 5 * L, 3 * cq2);
     lin_add<F>(acc, a + k * E2 + im * L, (k & 1) ? 2 : -2);
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -462,21 +483,40 @@ KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o) {
   __syncthreads();
 }
 
+// dst = a^p: coefficient k is conj(a_k) g_k (g_k = P::FROB[k]); lane (k, t)
+// < 24 forms one of the four Fp products of conj(a_k) g_k, lane (k, im) < 12
+// folds re = a.re g.re + a.im g.im, im = a.re g.im - a.im g.re
 template <class C>
-KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o) {
+KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
+  uint32_t* prod = vw_smem + prod_o;
   using P = typename PairOf<C>::T;
-  constexpr int E2 = VWave<C>::E2;
-  const int k = threadIdx.x;
-  if (k < 6) {
-    Fp2<C> g = f2_const<C>(P::FROB[0]);
-    if (k == 1) g = f2_const<C>(P::FROB[1]);
-    if (k == 2) g = f2_const<C>(P::FROB[2]);
-    if (k == 3) g = f2_const<C>(P::FROB[3]);
-    if (k == 4) g = f2_const<C>(P::FROB[4]);
-    if (k == 5) g = f2_const<C>(P::FROB[5]);
-    vw_st2<C>(dst + k * E2, f2_mul<C>(f2_conj<C>(vw_ld2<C>(a + k * E2)), g));
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  const int lane = threadIdx.x;
+  if (lane < 24) {
+    const int k = lane >> 2, t = lane & 3;
+    // t: 0 a.re g.re, 1 a.im g.im, 2 a.re g.im, 3 a.im g.re
+    F29<F> g;
+#pragma unroll
+    for (int l = 0; l < L; l++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int kk = 0; kk < 6; kk++) v = k == kk ? P::FROB[kk][(t == 1 || t == 2) ? 1 : 0][l] : v;
+      g.v[l] = v;
+    }
+    vw_st<C>(prod + lane * L, f29_mul<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    const int k = lane >> 1, im = lane & 1;
+    const uint32_t* q = prod + k * 4 * L;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add<F>(acc, q + (im ? 2 : 0) * L, 1);
+    lin_add<F>(acc, q + (im ? 3 : 1) * L, im ? -1 : 1);
+    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
   __syncthreads();
 }
@@ -539,7 +579,7 @@ KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
       case VW_MUL: vw_mul<C>(d, a, b, prod); break;
       case VW_CSQR: vw_cyclo_sqr<C>(d, a, prod); break;
       case VW_CONJ: vw_conj<C>(d, a); break;
-      case VW_FROB: vw_frob<C>(d, a); break;
+      case VW_FROB: vw_frob<C>(d, a, prod); break;
       case VW_INV: vw_inv<C>(d, a); break;
       default: {  // d = a^e (cyclotomic a, top bit of e set), d != a
         uint64_t e0 = op[3], e1 = 0;
@@ -711,7 +751,7 @@ KZGX_DEV void vl_dbl_wave(uint32_t* out) {
         break;
       default: lin_add<F>(acc, vl_comp<C>(S::YZ, im), 2); break;
     }
-    const F29<F> v = lin_fin_wide<F>(acc);
+    const F29<F> v = lin_fin<F>(acc);
     if (w < 3) {
       vw_st<C>(out + w * E2 + im * L, v);
     } else {
@@ -970,8 +1010,10 @@ KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __rest
     *ok_out = bad == 0 ? 1u : 0u;
 #ifdef KZGX_VW_TIMING
     if (blockIdx.x == 0)
-      printf("vw_ts tree %llu d %llu scale %llu miller %llu final_exp %llu (x10ns)\n", vw_ts[1] - vw_ts[0],
-             vw_ts[2] - vw_ts[1], vw_ts[3] - vw_ts[2], vw_ts[4] - vw_ts[3], vw_ts[8] - vw_ts[4]);
+      printf("vw_ts tree %llu d %llu scale %llu miller %llu final_exp %llu (x10ns)\n",
+             (unsigned long long)(vw_ts[1] - vw_ts[0]), (unsigned long long)(vw_ts[2] - vw_ts[1]),
+             (unsigned long long)(vw_ts[3] - vw_ts[2]), (unsigned long long)(vw_ts[4] - vw_ts[3]),
+             (unsigned long long)(vw_ts[8] - vw_ts[4]));
 #endif
   }
 }
@@ -1090,20 +1132,31 @@ size_t verify_wave_bytes(int curve) {
   return 4 * (curve == KZGX_CURVE_BN254 ? vw_buf_words<BN254G1>() : vw_buf_words<BLS12381G1>());
 }
 
+// at setup (both SRS halves present): the [y]G table (a copy of the
+// generator's comb when G1[0] is the generator) and the line tables of
+// G2[0], G2[1] from the wave-parallel G2 chain (k_vlines_wave; a degenerate
+// chain is recomputed on one lane)
 template <class C>
-static int verify_wave_prepare_impl(const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st) {
+static int verify_wave_prepare_impl(const uint32_t* d_g1_0, const uint32_t* d_g2_01, const uint32_t* g1_comb,
+                                    uint32_t* d_buf, hipStream_t st) {
   uint32_t* lines = d_buf + vw_tab_words<C>();
   uint32_t* qfin = lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
-  hipLaunchKernelGGL(k_vtab<C>, dim3((VWave<C>::TAB + 63) / 64), dim3(64), 0, st, d_g1_0, d_buf);
-  hipLaunchKernelGGL(k_vlines<C>, dim3(1), dim3(64), 0, st, d_g2_01, lines, qfin);
+  if (g1_comb) {
+    KZGX_TRY(vtab_prepare(C::ID == 0 ? KZGX_CURVE_BN254 : KZGX_CURVE_BLS12381, d_g1_0, g1_comb, d_buf, st));
+  } else {
+    hipLaunchKernelGGL(k_vtab<C>, dim3((VWave<C>::TAB + 63) / 64), dim3(64), 0, st, d_g1_0, d_buf);
+  }
+  hipLaunchKernelGGL(k_vlines_wave<C>, dim3(2), dim3(64), VLine<C>::WORDS * 4, st, d_g2_01, lines, qfin, qfin + 2);
+  hipLaunchKernelGGL(k_vlines_redo<C>, dim3(1), dim3(64), 0, st, d_g2_01, lines, qfin + 2);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }
 
-int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, uint32_t* d_buf, hipStream_t st) {
+int verify_wave_prepare(Ctx* ctx, const uint32_t* d_g1_0, const uint32_t* d_g2_01, const uint32_t* g1_comb,
+                        uint32_t* d_buf, hipStream_t st) {
   ProfScope p(ctx, st, "verify_wave_prepare");
-  return ctx->curve == KZGX_CURVE_BN254 ? verify_wave_prepare_impl<BN254G1>(d_g1_0, d_g2_01, d_buf, st)
-                                        : verify_wave_prepare_impl<BLS12381G1>(d_g1_0, d_g2_01, d_buf, st);
+  return ctx->curve == KZGX_CURVE_BN254 ? verify_wave_prepare_impl<BN254G1>(d_g1_0, d_g2_01, g1_comb, d_buf, st)
+                                        : verify_wave_prepare_impl<BLS12381G1>(d_g1_0, d_g2_01, g1_comb, d_buf, st);
 }
 
 template <class C>
@@ -1154,4 +1207,14 @@ int pair2_wave(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uin
                                         : pair2_wave_impl<BLS12381G1>(d_p, d_p_inf, d_q, d_q_inf, d_scratch, d_ok, st);
 }
 
+}  // namespace kzgx
+
+namespace kzgx {
+// device bring-up (kzgx_setup.hpp): one launch loads this code object
+__global__ void k_warm_verify_wave() {}
+int warm_verify_wave(hipStream_t st) {
+  hipLaunchKernelGGL(k_warm_verify_wave, dim3(1), dim3(64), 0, st);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
 }  // namespace kzgx

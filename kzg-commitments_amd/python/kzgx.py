@@ -20,14 +20,14 @@ BASE_LIMBS = {"BN254": 4, "BLS12381": 6}
 
 # exported C symbols (must match include/kzg_gpu.h)
 EXPORTS = [
-    "kzgx_strerror", "kzgx_base_limbs", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
+    "kzgx_strerror", "kzgx_base_limbs", "kzgx_init_device", "kzgx_create", "kzgx_destroy", "kzgx_sync", "kzgx_curve",
     "kzgx_srs_size", "kzgx_stream", "kzgx_prof_enable", "kzgx_prof_read", "kzgx_prof_clear", "kzgx_set_window_bits", "kzgx_set_segment",
     "kzgx_set_fixed_base", "kzgx_fixed_base_info", "kzgx_fixed_base_bytes", "kzgx_set_fixed_base_budget",
     "kzgx_set_fixed_base_layout", "kzgx_fixed_base_layout", "kzgx_set_default_table", "kzgx_default_table_info",
     "kzgx_microbench_mad_u64", "kzgx_microbench_mad_u64_clock", "kzgx_clock_probe", "kzgx_set_fixed_points_per_thread", "kzgx_set_small_batch", "kzgx_microbench_mixed_add", "kzgx_load_srs_g1", "kzgx_gen_srs_g1", "kzgx_get_srs_g1", "kzgx_msm_g1",
     "kzgx_msm_g1_batch", "kzgx_msm_g1_batch_device", "kzgx_quotient_single_batch_device",
     "kzgx_prove_single_batch", "kzgx_prove_single_batch_device", "kzgx_prove_range", "kzgx_poly_eval",
-    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device",
+    "kzgx_poly_interpolate", "kzgx_poly_vanishing", "kzgx_g1_validate", "kzgx_g1_sum", "kzgx_g1_sum_device", "kzgx_g1_sum_packed_device",
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
     "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max", "kzgx_msm_g1_sharded",
@@ -65,6 +65,7 @@ def lib():
         sig = {
             "kzgx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
             "kzgx_base_limbs": (ctypes.c_int, [ctypes.c_int]),
+            "kzgx_init_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
             "kzgx_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int]),
             "kzgx_destroy": (None, [vp]),
             "kzgx_sync": (ctypes.c_int, [vp]),
@@ -107,6 +108,7 @@ def lib():
             "kzgx_g1_validate": (ctypes.c_int, [vp, u64p, intp]),
             "kzgx_g1_sum": (ctypes.c_int, [vp, u64p, intp, sz, u64p, intp]),
             "kzgx_g1_sum_device": (ctypes.c_int, [vp, vp, vp, sz, vp, vp, vp]),
+            "kzgx_g1_sum_packed_device": (ctypes.c_int, [vp, vp, sz, vp, vp]),
             "kzgx_gen_srs_g2": (ctypes.c_int, [vp, u64p, sz, sz]),
             "kzgx_load_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
             "kzgx_get_srs_g2": (ctypes.c_int, [vp, u64p, sz]),
@@ -420,6 +422,15 @@ class Context:
                       stream: int | None = None):
         """Fold of count device-resident canonical points (uint32 infinity flags) on stream."""
         _chk(lib().kzgx_g1_sum_device(self.h, d_xy, d_inf, count, d_out, d_out_inf, stream), "kzgx_g1_sum_device")
+
+    def g1_sum_packed_device(self, d_rec: int, count: int, d_out: int, stream: int | None = None):
+        """Fold of count packed records (2 W64 uint64 x || y, then a uint64 infinity word) into one
+        record at d_out, on stream (the sharded commitment's exchange format)."""
+        _chk(lib().kzgx_g1_sum_packed_device(self.h, d_rec, count, d_out, stream), "kzgx_g1_sum_packed_device")
+
+    def init_device(self=None, curve: str = "BN254", device: int = 0):
+        """kzgx_init_device: HIP, every code object and the generator tables, once."""
+        _chk(lib().kzgx_init_device(CURVES[curve], device), "kzgx_init_device")
 
     # ---- verify half: G2 setup, polyeval_G2, pairing ----
     # G2 points: (n, 4 * W64) uint64 = x.re || x.im || y.re || y.im; Fp12: (12 * W64,)

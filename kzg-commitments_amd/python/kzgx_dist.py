@@ -63,29 +63,33 @@ def sharded_commit(n: int, world: int, rank: int, w64: int,
 
 def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
                           partial_msm: Callable[[int, int], "object"],
-                          fold: Callable[["object", "object"], "object"],
+                          fold: Callable[["object"], "object"],
                           dist, torch, on_phase: Optional[Callable[[str], None]] = None) -> "object":
     """Device-resident form of sharded_commit (bench.py's configs[4] step).
 
-    partial_msm(start, count) -> this rank's packed partial (2 W64 + 1 int64:
-    x || y || infinity flag) as a tensor on the compute device, enqueued with
-    no host synchronisation; the packed partials are all-gathered (RCCL over
-    xGMI on GPU, gloo on CPU) straight into device tensors; fold(points
-    (world, 2 W64) int64, flags (world,) int32) -> packed result tensor.
-    Nothing crosses to the host inside a step.  on_phase(name), if given, is
-    called after each phase is enqueued ("partial", "gather", "fold"), e.g.
-    to record timing events on the step's stream."""
+    partial_msm(start, count) -> this rank's packed record (2 W64 + 1 int64:
+    x || y || infinity word) as a tensor on the compute device, enqueued with
+    no host synchronisation; the records are all-gathered (RCCL over xGMI on
+    GPU, gloo on CPU) straight into one (world, 2 W64 + 1) tensor, and
+    fold(records) -> the packed sum (kzgx_g1_sum_packed_device on the GPU).
+    Nothing crosses to the host inside a step, and nothing is repacked
+    between the phases.  on_phase(name), if given, is called after each phase
+    is enqueued ("partial", "gather", "fold"), e.g. to record timing events
+    on the step's stream."""
     mark = on_phase or (lambda _name: None)
     start, count = shard_range(n, world, rank)
     packed = partial_msm(start, count)
     mark("partial")
     if world == 1:
         return packed
-    outs = [torch.empty_like(packed) for _ in range(world)]
-    dist.all_gather(outs, packed)
-    g = torch.stack(outs)
+    g = torch.empty((world, packed.shape[0]), dtype=packed.dtype, device=packed.device)
+    if hasattr(dist, "all_gather_into_tensor") and packed.device.type == "cuda":
+        dist.all_gather_into_tensor(g, packed)
+    else:  # gloo has no all_gather_into_tensor
+        outs = list(g.unbind(0))
+        dist.all_gather(outs, packed)
     mark("gather")
-    res = fold(g[:, : 2 * w64].contiguous(), g[:, 2 * w64].to(torch.int32).contiguous())
+    res = fold(g)
     mark("fold")
     return res
 

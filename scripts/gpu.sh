@@ -14,6 +14,8 @@
 #   pmc:CTRS[:ARGS]   one rocprofv3 --pmc pass (CTRS comma-separated) around bench.py ARGS
 #   py:SCRIPT[,ARGS]  python3 scripts/SCRIPT ARGS
 #   profpy:SCRIPT[,ARGS] rocprofv3 --kernel-trace --stats around python3 scripts/SCRIPT ARGS
+#   bin:PATH[,ARGS]   a built binary (e.g. kzg-commitments_amd/tools/kzg_bench)
+#   profbin:PATH[,ARGS] rocprofv3 --kernel-trace --stats around a built binary
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 TAG=$1
@@ -79,6 +81,17 @@ for st in "$@"; do
         -- python3 -u "scripts/$1" "${@:2}" > "$OUT/profpy_$n.txt" 2>&1 \
         || { tail -20 "$OUT/profpy_$n.txt"; exit 1; }
       tail -12 "$OUT/profpy_$n.txt"
+      ;;
+    bin)
+      set -- ${arg//,/ }
+      timeout -k 10 600 "./$1" "${@:2}" > "$OUT/bin_$n.txt" 2>&1 || { tail -20 "$OUT/bin_$n.txt"; exit 1; }
+      tail -20 "$OUT/bin_$n.txt"
+      ;;
+    profbin)
+      set -- ${arg//,/ }
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbin_$n" -o prof --output-format csv \
+        -- "./$1" "${@:2}" > "$OUT/profbin_$n.txt" 2>&1 || { tail -20 "$OUT/profbin_$n.txt"; exit 1; }
+      tail -12 "$OUT/profbin_$n.txt"
       ;;
     *)
       echo "unknown step $st"

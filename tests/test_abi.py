@@ -54,6 +54,15 @@ def test_no_device_means_no_compute():
     assert e.value.status == -7  # KZGX_ERR_NO_DEVICE
 
 
+def test_init_device_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import kzgx
+    assert kzgx.lib().kzgx_init_device(0, 0) == -7  # KZGX_ERR_NO_DEVICE
+    assert kzgx.lib().kzgx_init_device(9, 0) == -1  # unknown curve, before any device query
+
+
 def test_bad_arguments_rejected_before_device():
     import kzgx
     h = ctypes.c_void_p()

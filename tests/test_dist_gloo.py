@@ -54,16 +54,18 @@ def _worker(rank, world, port, n, results):
     results[rank] = got
 
     # the device-resident driver (bench.py's configs[4] step) on CPU tensors:
-    # packed partials, all-gather into tensors, fold over (points, int32 flags)
+    # packed records, all-gathered into one (world, 2 W64 + 1) tensor, folded
+    # as records (the format kzgx_g1_sum_packed_device reads)
     import torch
 
     def partial_t(start, count):
         xy, inf = partial(start, count)
         return torch.from_numpy(kzgx_dist.pack_point(xy, inf, 4))
 
-    def fold_t(pts, flags):
-        assert pts.dtype == torch.int64 and flags.dtype == torch.int32 and pts.shape == (world, 8)
-        acc, inf = fold(pts.numpy().view(np.uint64), flags.numpy() != 0)
+    def fold_t(recs):
+        assert recs.dtype == torch.int64 and recs.shape == (world, 9)
+        pts, infs = kzgx_dist.unpack_points(recs.numpy(), 4)
+        acc, inf = fold(pts, infs)
         xy = np.zeros(8, dtype=np.uint64)
         if acc is not None:
             for j in range(4):

@@ -122,3 +122,85 @@ def test_sparse_and_small_scalars(name, C):
         assert as_point(name, out, inf) == K.commit_via_tau(C, tau, sc)
     finally:
         ctx.close()
+
+
+# ---- the wide-window single-MSM path (msm.hip msm_big, round 5) ----------------
+# An SRS of >= 2^16 points gets a wide-window table at setup: c = 14 below
+# 2^17 points, 15 below 2^18, 16 from there; single MSMs of >= 2^16 points
+# take it (global counting sort, LDS histograms of 2^(c-1) buckets, the
+# batched accumulation / merges, latency.hip's bucket reduction).
+BIG = [(65536 + 7, 14), (131072 + 3, 15), (262144 + 1, 16)]
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("srs_n,cbits", BIG)
+def test_big_window_random_and_edges(name, C, srs_n, cbits):
+    """random scalars with zeros, r - 1, 1 and 2^k values mixed in, at the
+    SRS size and one below; and the shortest MSM that takes the path"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        tau = K.default_tau(C)
+        ctx.gen_srs(tau, srs_n)
+        for n in (srs_n, srs_n - 1, 65536):
+            sc = K.random_scalars(C, n, seed=n + cbits)
+            for j in range(0, n, 997):
+                sc[j] = 0
+            sc[1], sc[2], sc[3], sc[n - 1] = C.r - 1, 1, 1 << 200, (1 << 255) % C.r
+            out, inf = ctx.msm(limbs(sc))
+            assert as_point(name, out, inf) == K.commit_via_tau(C, tau, sc), n
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("srs_n,cbits", BIG)
+def test_big_window_one_giant_bucket(name, C, srs_n, cbits):
+    """all scalars equal: every window's entries in one bucket spanning
+    thousands of segments and many merge workgroups"""
+    import kzgx
+    ctx = kzgx.Context(name)
+    try:
+        tau = K.default_tau(C)
+        ctx.gen_srs(tau, srs_n)
+        s = K.random_scalars(C, 1, seed=cbits)[0]
+        sc = [s] * srs_n
+        out, inf = ctx.msm(limbs(sc))
+        assert as_point(name, out, inf) == K.commit_via_tau(C, tau, sc)
+        # the top bucket (digit 2^(c-1) in every window below the top)
+        top = sum((1 << (cbits - 1)) << (cbits * w) for w in range(256 // cbits)) % C.r
+        sc = [top] * 65536
+        out, inf = ctx.msm(limbs(sc))
+        assert as_point(name, out, inf) == K.commit_via_tau(C, tau, sc)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_big_window_degenerate_setups(name, C):
+    """tau = 1 (every point G: s and r - s cancel bucket by bucket; one extra
+    term survives) and tau = 0 (every point but the first is infinite)"""
+    import kzgx
+    n = 65536 + 2
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(1, n)
+        base = K.random_scalars(C, n // 2, seed=5)
+        sc = []
+        for v in base:
+            sc += [v, (C.r - v) % C.r]
+        out, inf = ctx.msm(limbs(sc))
+        assert inf and not out.any()
+        sc[77] = (sc[77] + 5) % C.r
+        out, inf = ctx.msm(limbs(sc))
+        assert as_point(name, out, inf) == K.commit_via_tau(C, 1, sc)
+    finally:
+        ctx.close()
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(0, n)
+        sc = K.random_scalars(C, n, seed=6)
+        out, inf = ctx.msm(limbs(sc))
+        assert as_point(name, out, inf) == K.commit_via_tau(C, 0, sc)
+    finally:
+        ctx.close()

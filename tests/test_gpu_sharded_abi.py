@@ -64,3 +64,53 @@ def test_msm_g1_sharded(name, C):
     finally:
         for c in ctxs + [whole]:
             c.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+@pytest.mark.parametrize("count", [1, 2, 3, 8, 64, 65, 130])
+def test_g1_sum_packed_device(name, C, count):
+    """kzgx_g1_sum_packed_device: the sharded commitment's one-wave fold over
+    packed records (x || y || infinity word), against the oracle sum; with
+    infinite records, a record equal to another (doubling) and one cancelling
+    another (P + (-P))."""
+    import torch
+    import kzgx
+    tau = K.default_tau(C)
+    w = 4 if C is K.BN254 else 6
+    ctx = kzgx.Context(name)
+    try:
+        ctx.gen_srs(tau, 4)
+        rng = np.random.default_rng(count)
+        ks = [int(rng.integers(1, 1 << 62)) for _ in range(count)]
+        if count >= 3:
+            ks[1] = ks[0]                  # equal records: the fold doubles
+            ks[2] = C.r - ks[0] if count > 3 else ks[2]  # P and -P cancel
+        infs = [count > 4 and j % 5 == 4 for j in range(count)]
+        rec = np.zeros((count, 2 * w + 1), dtype=np.uint64)
+        exp = None
+        for j, (k, inf) in enumerate(zip(ks, infs)):
+            if inf:
+                rec[j, -1] = 1
+                continue
+            x, y = K.scalar_mul(C, (C.gx, C.gy), k)
+            for i in range(w):
+                rec[j, i] = (x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+                rec[j, w + i] = (y >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+            exp = K.point_add(C, exp, (x, y))
+        d_rec = torch.from_numpy(rec.view(np.int64)).cuda()
+        d_out = torch.full((2 * w + 1,), -1, dtype=torch.int64, device="cuda")
+        ctx.g1_sum_packed_device(d_rec.data_ptr(), count, d_out.data_ptr())
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy().view(np.uint64)
+        got = None if out[-1] else point(C, out[: 2 * w], False)
+        assert int(out[-1]) in (0, 1)
+        assert got == exp
+    finally:
+        ctx.close()
+
+
+def test_init_device_twice():
+    """kzgx_init_device (kzg::init's device bring-up) is idempotent per process."""
+    import kzgx
+    for curve in ("BN254", "BLS12381", "BN254"):
+        assert kzgx.lib().kzgx_init_device(kzgx.CURVES[curve], 0) == 0
