@@ -157,9 +157,11 @@ KZGX_DEV F29<F> f29_mul_lat(const F29<F>& a, const F29<F>& b) {
 #pragma unroll
   for (int k = 0; k < L; k++) {
     const uint32_t q = ((uint32_t)col[k] * F::INV) & M29;
-    col[k + 1] += (col[k] + (uint64_t)q * F::P[0]) >> 29;
+    // modulus limbs as opaque uniform values (f29_pl): one v_mad_u64_u32
+    // each, never strength-reduced to shifts and adds
+    col[k + 1] += (col[k] + (uint64_t)q * f29_pl<F>(0)) >> 29;
 #pragma unroll
-    for (int j = 1; j < L; j++) col[k + j] += (uint64_t)q * F::P[j];
+    for (int j = 1; j < L; j++) col[k + j] += (uint64_t)q * f29_pl<F>(j);
   }
   F29<F> t;
   uint64_t c = 0;
@@ -170,6 +172,42 @@ KZGX_DEV F29<F> f29_mul_lat(const F29<F>& a, const F29<F>& b) {
     c = s >> 29;
   }
   t.v[L - 1] = (uint32_t)c;
+  return t;
+}
+
+// (a b + c d) / R, latency-first (f29_mul2's value and bounds): column
+// sums 2L products + L reduction terms < 2^58 each, < 2^64 for both curves
+template <class F>
+KZGX_DEV F29<F> f29_mul2_lat(const F29<F>& a, const F29<F>& b, const F29<F>& c, const F29<F>& d) {
+  constexpr int L = F::L;
+  uint64_t col[2 * L];
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) s += (uint64_t)a.v[i] * b.v[j] + (uint64_t)c.v[i] * d.v[j];
+    }
+    col[k] = s;
+  }
+  col[2 * L - 1] = 0;
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    const uint32_t q = ((uint32_t)col[k] * F::INV) & M29;
+    col[k + 1] += (col[k] + (uint64_t)q * f29_pl<F>(0)) >> 29;
+#pragma unroll
+    for (int j = 1; j < L; j++) col[k + j] += (uint64_t)q * f29_pl<F>(j);
+  }
+  F29<F> t;
+  uint64_t cy = 0;
+#pragma unroll
+  for (int k = L; k < 2 * L - 1; k++) {
+    const uint64_t s = col[k] + cy;
+    t.v[k - L] = (uint32_t)s & M29;
+    cy = s >> 29;
+  }
+  t.v[L - 1] = (uint32_t)cy;
   return t;
 }
 
@@ -216,6 +254,9 @@ KZGX_DEV F29<F> f29_mul(const F29<F>& a, const F29<F>& b) {
 // Output < 2m when a b + c d < (R / m) m^2.
 template <class F>
 KZGX_DEV F29<F> f29_mul2(const F29<F>& a, const F29<F>& b, const F29<F>& c, const F29<F>& d) {
+#ifdef KZGX_FIELD_LATENCY
+  return f29_mul2_lat<F>(a, b, c, d);
+#endif
   constexpr int L = F::L;
   uint32_t q[L];
   F29<F> t;

@@ -534,17 +534,21 @@ int kzgx_msm_g1_batch(kzgx_ctx* ctx, const uint64_t* scalars, size_t n, size_t b
   if (n > ctx->c.n_srs) return KZGX_ERR_DEGREE;
   const size_t sb = n * batch * 32, ob = batch * point_words(ctx) * 4;
   // pinned layout: [results | flags | scalars]; results are written by the
-  // last kernel into mapped host memory (no D2H copy)
+  // last kernel into mapped host memory (no D2H copy).  Scalars up to
+  // PIN_DIRECT_MAX are read by the kernels from the pinned copy; larger
+  // ones are DMA'd straight from the caller's buffer (no host copy, and the
+  // pinned buffer stays small: ADVICE r04)
+  const bool direct = sb <= PIN_DIRECT_MAX;
   const size_t o_off = 0, i_off = align256(ob), s_off = i_off + align256(batch * 4);
-  KZGX_TRY(pin_stage(ctx, s_off + sb));
+  KZGX_TRY(pin_stage(ctx, s_off + (direct ? sb : 0)));
   void* d_s = nullptr;
   if (n) {
-    std::memcpy(ctx->h_pin + s_off, scalars, sb);
-    if (sb <= PIN_DIRECT_MAX) {
+    if (direct) {
+      std::memcpy(ctx->h_pin + s_off, scalars, sb);
       d_s = ctx->d_pin + s_off;
     } else {
       KZGX_TRY(stage(ctx, 0, sb, &d_s));
-      KZGX_TRY_HIP(hipMemcpyAsync(d_s, ctx->h_pin + s_off, sb, hipMemcpyHostToDevice, ctx->c.stream));
+      KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, ctx->c.stream));
     }
   }
   KZGX_TRY(kzgx_msm_g1_batch_device(ctx, d_s, n, batch, n, ctx->d_pin + o_off, ctx->d_pin + i_off, nullptr));
@@ -673,18 +677,19 @@ int kzgx_prove_single_batch(kzgx_ctx* ctx, const uint64_t* coeffs, size_t n, siz
   const size_t ob = batch * point_words(ctx) * 4;
   // pinned layout: [results | flags | y | z | coefficients]; outputs are
   // written by the kernels into mapped host memory (no D2H copies)
+  const bool direct = cb <= PIN_DIRECT_MAX;  // as kzgx_msm_g1_batch
   const size_t o_off = 0, i_off = align256(ob), y_off = i_off + align256(batch * 4),
                z_off = y_off + align256(batch * 32), c_off = z_off + align256(batch * 32);
-  KZGX_TRY(pin_stage(ctx, c_off + cb));
+  KZGX_TRY(pin_stage(ctx, c_off + (direct ? cb : 0)));
   std::memcpy(ctx->h_pin + z_off, zs, batch * 32);
   void* d_c = nullptr;
   if (n) {
-    std::memcpy(ctx->h_pin + c_off, coeffs, cb);
-    if (cb <= PIN_DIRECT_MAX) {
+    if (direct) {
+      std::memcpy(ctx->h_pin + c_off, coeffs, cb);
       d_c = ctx->d_pin + c_off;
     } else {
       KZGX_TRY(stage(ctx, 0, cb, &d_c));
-      KZGX_TRY_HIP(hipMemcpyAsync(d_c, ctx->h_pin + c_off, cb, hipMemcpyHostToDevice, ctx->c.stream));
+      KZGX_TRY_HIP(hipMemcpyAsync(d_c, coeffs, cb, hipMemcpyHostToDevice, ctx->c.stream));
     }
   }
   KZGX_TRY(kzgx_prove_single_batch_device(ctx, d_c, n, coeff_stride, ctx->d_pin + z_off, batch, ctx->d_pin + o_off,
@@ -1197,4 +1202,13 @@ extern "C" int kzgx_debug_latency(kzgx_ctx* ctx, int op, unsigned iters, double*
   if (!res) return KZGX_ERR_ARG;
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
   return kzgx::debug_latency(&ctx->c, op, iters, res);
+}
+
+// debug: latency of one wave-wide Fp12 op of the verify path
+// (verify_wave.hip k_vw_bench): res[0] = ns per op, res[1] = core clocks
+extern "C" int kzgx_debug_vw_bench(kzgx_ctx* ctx, int op, unsigned iters, double* res) {
+  KZGX_TRY(activate(ctx));
+  if (!res || iters == 0) return KZGX_ERR_ARG;
+  KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  return kzgx::vw_bench(ctx->c.curve, op, iters, &res[0], &res[1], ctx->c.stream);
 }

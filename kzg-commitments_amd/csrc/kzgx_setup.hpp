@@ -61,6 +61,10 @@ int vtab_prepare(int curve, const uint32_t* d_g1_0, const uint32_t* g1_comb, uin
 // (x || y canonical words, then a 64-bit infinity word) summed into one
 int g1_fold_packed(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st);
 
+// latency of one wave-wide Fp12 op of the verify path (verify_wave.hip
+// k_vw_bench; kzgx_debug_vw_bench)
+int vw_bench(int curve, int op, uint32_t iters, double* ns_per_op, double* clk_per_op, hipStream_t st);
+
 // the bucket reduction of one wide-window Pippenger MSM (latency.hip):
 // sum_k (k + 1) B_k over nb >= 4096 buckets (bsum, occupancy from offsets)
 // -> canonical affine out / out_inf; d_rt: big_reduce_rt_bytes of scratch

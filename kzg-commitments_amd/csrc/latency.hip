@@ -40,7 +40,7 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
     const uint32_t* r = rec + (size_t)k * RW;
     Affine<C> a;
     const bool fin = affine_from_canonical<C>(r, a) && (r[2 * N] | r[2 * N + 1]) == 0u;
-    if (fin) acc = xyzz_add_affine<C>(acc, a);
+    if (fin) acc = xyzz_add_affine_impl<C>(acc, a);
   }
   for (int off = 32; off >= 1; off >>= 1) {
     if (count <= (uint32_t)off) continue;  // uniform: no lane >= off holds a record
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
       o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], off, 64);
       o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], off, 64);
     }
-    acc = xyzz_add<C>(acc, o);
+    acc = xyzz_add_impl<C>(acc, o);
   }
   // every lane holds a representative of the total; lane 0's is converted
   // by the whole wave (wave-uniform binary GCD on the scalar ALU)
@@ -67,18 +67,22 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
 
 // ---- bucket reduction of one wide-window Pippenger MSM (msm.hip, big path) ----
 // V = sum_k (k + 1) B_k over nb = 2^(c-1) buckets (c = 14..16), the chain
-// that follows the accumulation.  Depth matters more than work here (a few
-// waves per SIMD at most), hence this translation unit's product.
-//   k_lat_bucket_sums: thread t owns J buckets: R_t = sum_j (j+1) B_{tJ+j},
-//                      T_t = sum_j B_{tJ+j} (running sums, 2 J additions)
-//   k_lat_big_fold:    one 512-thread workgroup folds the T1 = nb / J pairs,
-//                      G = T1 / 512 per thread, with the algebra of msm.hip's
-//                      k_msm_bucket_fold_wg (suffix sums S_l of T' give
-//                      sum_l l T'_l), the wavefront totals scanned and summed
-//                      through LDS by log-depth shuffles, then wavefront 0
-//                      converts the total with the wave-uniform inversion.
-constexpr uint32_t BIG_RED_J = 8;
-constexpr uint32_t BIG_FOLD_T = 512;
+// that follows the accumulation.  Its depth is ~log2(nb) doublings plus
+// ~2 log2(nb) additions whatever the schedule, and a lone wave issues one
+// XYZZ addition in ~7 us (its ~2400 VALU instructions), so the schedule is
+// made wide: every level runs on as many waves as it has elements.
+//   k_lat_bucket_sums: thread t owns J = 2 buckets: R_t = B_{2t} + 2 B_{2t+1},
+//                      T_t = B_{2t} + B_{2t+1}  (nb / 2 threads)
+//   k_lat_fold1:       256-thread workgroup g over pairs t = 256 g + l:
+//                      V_g = sum_l R_l + J sum_l l T_l (suffix sums S_l of T
+//                      by a wave scan + the higher waves' totals, a tree),
+//                      T_g = sum_l T_l
+//   k_lat_fold2:       one wave over the NG = nb / 512 groups: V = sum_g V_g
+//                      + 256 J sum_g g T_g the same way, then the wave-uniform
+//                      affine conversion
+// (k_msm_bucket_fold_wg's algebra: sum_t t T_t = sum_{t >= 1} S_t.)
+constexpr uint32_t BIG_RED_J = 2;
+constexpr uint32_t BIG_F1 = 256;  // pairs per fold-1 workgroup
 
 template <class C>
 __global__ __launch_bounds__(256) void k_lat_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb,
@@ -90,10 +94,9 @@ __global__ __launch_bounds__(256) void k_lat_bucket_sums(const uint32_t* __restr
   const uint32_t* off = offsets + (size_t)t * J;
   const uint32_t* src = bsum + (size_t)t * J * XW;
   Xyzz<C> run = xyzz_inf<C>(), sum = xyzz_inf<C>();
-#pragma unroll 1
   for (int j = (int)J - 1; j >= 0; j--) {
-    if (off[j + 1] > off[j]) run = xyzz_add<C>(run, xyzz_load<C>(src + (size_t)j * XW));  // empty: never written
-    sum = xyzz_add<C>(sum, run);
+    if (off[j + 1] > off[j]) run = xyzz_add_impl<C>(run, xyzz_load<C>(src + (size_t)j * XW));  // empty: never written
+    sum = xyzz_add_impl<C>(sum, run);
   }
   xyzz_store<C>(rt + (size_t)t * 2 * XW, sum);
   xyzz_store<C>(rt + (size_t)t * 2 * XW + XW, run);
@@ -115,73 +118,76 @@ KZGX_DEV Xyzz<C> xyzz_shfl_down_w(const Xyzz<C>& p, int off) {
 template <class C>
 KZGX_DEV Xyzz<C> xyzz_dbl_pow2(Xyzz<C> p, uint32_t m) {  // m p, m a power of two
 #pragma unroll 1
-  for (; m > 1; m >>= 1) p = xyzz_dbl<C>(p);
+  for (; m > 1; m >>= 1) p = xyzz_dbl_impl<C>(p);
   return p;
 }
 
+// inclusive suffix sums over the wave's lanes < n (lanes >= n: infinity)
 template <class C>
-__global__ __launch_bounds__(BIG_FOLD_T) void k_lat_big_fold(const uint32_t* __restrict__ rt, uint32_t T1,
-                                                             uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+KZGX_DEV Xyzz<C> wave_suffix(Xyzz<C> S, uint32_t lane, uint32_t n) {
+#pragma unroll 1
+  for (uint32_t o = 1; o < n; o <<= 1) {
+    const Xyzz<C> x = xyzz_shfl_down_w<C>(S, (int)o);
+    if (lane + o < n) S = xyzz_add_impl<C>(S, x);
+  }
+  return S;
+}
+// sum over the wave's lanes < n, landing in lane 0
+template <class C>
+KZGX_DEV Xyzz<C> wave_total(Xyzz<C> U, uint32_t n) {
+#pragma unroll 1
+  for (uint32_t o = 32; o >= 1; o >>= 1)
+    if (o < n) U = xyzz_add_impl<C>(U, xyzz_shfl_down_w<C>(U, (int)o));
+  return U;
+}
+
+template <class C>
+__global__ __launch_bounds__(BIG_F1) void k_lat_fold1(const uint32_t* __restrict__ rt, uint32_t* __restrict__ vt) {
   constexpr int XW = xyzz_words<C>();
-  constexpr uint32_t NW = BIG_FOLD_T / 64;  // wavefronts
-  constexpr uint32_t J = BIG_RED_J;
-  __shared__ uint32_t lds[2 * NW * XW];
+  constexpr uint32_t NW = BIG_F1 / 64;
+  __shared__ uint32_t lds[NW * XW];
   const uint32_t l = threadIdx.x, lane = l & 63, wv = l >> 6;
-  const uint32_t G = T1 / BIG_FOLD_T;
-  const uint32_t* src = rt + (size_t)l * G * 2 * XW;
-  // lane-local: R'_l = sum_i R_{lG+i} + J sum_i i T_{lG+i}, T'_l = sum_i T_{lG+i}
-  Xyzz<C> R = xyzz_load<C>(src + (size_t)(G - 1) * 2 * XW);
-  Xyzz<C> run = xyzz_load<C>(src + (size_t)(G - 1) * 2 * XW + XW);
-  Xyzz<C> acc = xyzz_inf<C>();
-#pragma unroll 1
-  for (int i = (int)G - 2; i >= 0; i--) {
-    acc = xyzz_add<C>(acc, run);
-    R = xyzz_add<C>(R, xyzz_load<C>(src + (size_t)i * 2 * XW));
-    run = xyzz_add<C>(run, xyzz_load<C>(src + (size_t)i * 2 * XW + XW));
-  }
-  if (G > 1) R = xyzz_add<C>(R, xyzz_dbl_pow2<C>(acc, J));
-  // inclusive suffix scan of T' over the workgroup: within the wavefront,
-  // then the exclusive suffix of the higher wavefronts' totals
-  Xyzz<C> S = run;
-#pragma unroll 1
-  for (int o = 1; o < 64; o <<= 1) {
-    const Xyzz<C> x = xyzz_shfl_down_w<C>(S, o);
-    if (lane + o < 64) S = xyzz_add<C>(S, x);
-  }
+  const uint32_t* src = rt + ((size_t)blockIdx.x * BIG_F1 + l) * 2 * XW;
+  const Xyzz<C> R = xyzz_load<C>(src);
+  Xyzz<C> S = wave_suffix<C>(xyzz_load<C>(src + XW), lane, 64);
   if (lane == 0) xyzz_store<C>(lds + wv * XW, S);
   __syncthreads();
-  if (wv == 0) {
-    Xyzz<C> tot = lane < NW ? xyzz_load<C>(lds + lane * XW) : xyzz_inf<C>();
 #pragma unroll 1
-    for (uint32_t o = 1; o < NW; o <<= 1) {
-      const Xyzz<C> x = xyzz_shfl_down_w<C>(tot, o);
-      if (lane + o < NW) tot = xyzz_add<C>(tot, x);
-    }
-    // exclusive: wavefront w adds the totals of w + 1 .. NW - 1
-    const Xyzz<C> nxt = xyzz_shfl_down_w<C>(tot, 1);
-    if (lane < NW) xyzz_store<C>(lds + (NW + lane) * XW, lane + 1 < NW ? nxt : xyzz_inf<C>());
-  }
-  __syncthreads();
-  if (wv + 1 < NW) S = xyzz_add<C>(S, xyzz_load<C>(lds + (NW + wv) * XW));
+  for (uint32_t w = wv + 1; w < NW; w++) S = xyzz_add_impl<C>(S, xyzz_load<C>(lds + w * XW));
+  const Xyzz<C> Tg = S;  // thread 0: the group total
   __syncthreads();  // lds is reused below
   Xyzz<C> U = R;
-  if (l > 0) U = xyzz_add<C>(U, xyzz_dbl_pow2<C>(S, J * G));
-#pragma unroll 1
-  for (int o = 32; o >= 1; o >>= 1) U = xyzz_add<C>(U, xyzz_shfl_down_w<C>(U, o));
+  if (l > 0) U = xyzz_add_impl<C>(U, xyzz_dbl_pow2<C>(S, BIG_RED_J));
+  U = wave_total<C>(U, 64);
   if (lane == 0) xyzz_store<C>(lds + wv * XW, U);
   __syncthreads();
-  if (wv != 0) return;
-  U = lane < NW ? xyzz_load<C>(lds + lane * XW) : xyzz_inf<C>();
+  if (l != 0) return;
 #pragma unroll 1
-  for (uint32_t o = NW / 2; o >= 1; o >>= 1) U = xyzz_add<C>(U, xyzz_shfl_down_w<C>(U, o));
-  // wavefront 0 converts lane 0's total (wave-uniform binary GCD)
+  for (uint32_t w = 1; w < NW; w++) U = xyzz_add_impl<C>(U, xyzz_load<C>(lds + w * XW));
+  xyzz_store<C>(vt + (size_t)blockIdx.x * 2 * XW, U);
+  xyzz_store<C>(vt + (size_t)blockIdx.x * 2 * XW + XW, Tg);
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void k_lat_fold2(const uint32_t* __restrict__ vt, uint32_t NG,
+                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t lane = threadIdx.x;
+  Xyzz<C> V = xyzz_inf<C>(), S = xyzz_inf<C>();
+  if (lane < NG) {
+    V = xyzz_load<C>(vt + (size_t)lane * 2 * XW);
+    S = xyzz_load<C>(vt + (size_t)lane * 2 * XW + XW);
+  }
+  S = wave_suffix<C>(S, lane, NG);
+  if (lane > 0 && lane < NG) V = xyzz_add_impl<C>(V, xyzz_dbl_pow2<C>(S, BIG_RED_J * BIG_F1));
+  V = wave_total<C>(V, NG);
   Xyzz<C> v;
 #pragma unroll
   for (int k = 0; k < C::Fp29::L; k++) {
-    v.X.v[k] = __builtin_amdgcn_readfirstlane(U.X.v[k]);
-    v.Y.v[k] = __builtin_amdgcn_readfirstlane(U.Y.v[k]);
-    v.ZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZ.v[k]);
-    v.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZZ.v[k]);
+    v.X.v[k] = __builtin_amdgcn_readfirstlane(V.X.v[k]);
+    v.Y.v[k] = __builtin_amdgcn_readfirstlane(V.Y.v[k]);
+    v.ZZ.v[k] = __builtin_amdgcn_readfirstlane(V.ZZ.v[k]);
+    v.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(V.ZZZ.v[k]);
   }
   Affine<C> a;
   const bool fin = xyzz_to_affine_impl<C, true>(v, a);
@@ -192,16 +198,19 @@ __global__ __launch_bounds__(BIG_FOLD_T) void k_lat_big_fold(const uint32_t* __r
 
 size_t big_reduce_rt_bytes(int curve, uint32_t nb) {
   const size_t xb = 4 * (curve == KZGX_CURVE_BN254 ? xyzz_words<BN254G1>() : xyzz_words<BLS12381G1>());
-  return (size_t)(nb / BIG_RED_J) * 2 * xb;
+  const size_t T1 = nb / BIG_RED_J;
+  return (T1 + T1 / BIG_F1) * 2 * xb;
 }
 
 template <class C>
 static int big_reduce_impl(const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
                            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
-  const uint32_t T1 = nb / BIG_RED_J;
-  if (T1 < BIG_FOLD_T || T1 % BIG_FOLD_T) return KZGX_ERR_INTERNAL;  // nb >= 4096
+  const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
+  if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb in [512, 2^15]
+  uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
   hipLaunchKernelGGL(k_lat_bucket_sums<C>, dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum, d_rt);
-  hipLaunchKernelGGL(k_lat_big_fold<C>, dim3(1), dim3(BIG_FOLD_T), 0, st, d_rt, T1, d_out, d_out_inf);
+  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(NG), dim3(BIG_F1), 0, st, d_rt, vt);
+  hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }

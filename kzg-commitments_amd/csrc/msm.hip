@@ -805,11 +805,11 @@ static size_t big_min_points() {
   return v ? v : ~(size_t)0;
 }
 // its window for an SRS of n points: fewer additions per point (n W) against
-// a longer bucket reduction (2^(c-1) buckets); KZGX_BIG_WINDOW pins it
+// a deeper bucket reduction (log2 of 2^(c-1) buckets); KZGX_BIG_WINDOW pins it
 static int big_window_bits(size_t n) {
   static const int pin = std::getenv("KZGX_BIG_WINDOW") ? std::atoi(std::getenv("KZGX_BIG_WINDOW")) : 0;
   if (pin >= 14 && pin <= 16) return pin;
-  return n >= ((size_t)1 << 18) ? 16 : n >= ((size_t)1 << 17) ? 15 : 14;
+  return n >= ((size_t)1 << 18) ? 16 : 14;
 }
 
 template <class C>
@@ -1030,10 +1030,10 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   const size_t emax = (size_t)n * W;
-  // count / scatter blocks of `per` scalars: ~128 blocks (their histograms,
-  // NB words each, are the scan's input)
-  uint32_t per = 2048;
-  while ((n + per - 1) / per > 128) per <<= 1;
+  // count / scatter blocks of 2048 scalars: each thread ranks two scalars'
+  // digits, so the LDS-atomic -> store chains stay short (~128 blocks of 8192
+  // measured 215 us for the 2^20 scatter); the scan reads nblk NB counters
+  const uint32_t per = 2048;
   const size_t nblk = (n + per - 1) / per;
   uint32_t K = ctx->seg_k;
   while (K > 8 && emax / K < 131072) K >>= 1;
@@ -1123,7 +1123,9 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
   {
     const FixedTable& d = ctx->fixed_def;
     const int min_c = ctx->curve == KZGX_CURVE_BN254 ? KZGX_DEFAULT_TABLE_BATCH_MIN_C_BN : KZGX_DEFAULT_TABLE_BATCH_MIN_C_BLS;
-    if (fixed_table_usable(d, n) && (batch <= ctx->small_batch || d.c >= min_c))
+    // batch <= 16: the latency kernel (fixed_msm_impl), whatever the
+    // small-window Pippenger knob (kzgx_set_small_batch) says
+    if (fixed_table_usable(d, n) && (batch <= 16 || d.c >= min_c))
       return fixed_msm_table(ctx, ctx->fixed_def, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, nullptr);
   }
 // Single MSMs chunk from 2^17 points: below, one un-chunked Pippenger (the

@@ -356,16 +356,19 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   }
   __syncthreads();
   if (lane < 12) {
+    // c_k = sum_i a_i a_{(k - i) mod 6} (xi for the wrapped ones): one
+    // uniform pass over i, reading the unordered pair's parts -- a cross
+    // pair (i, j) is met at i and at j, so it counts twice (the lanes'
+    // divergent walk over i <= j executed the union: twice the loads)
     const int k = lane >> 1, im = lane & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
-    for (int w = 0; w < 2; w++) {
-      const int sum = k + 6 * w;
-      for (int i = 0; i < 6; i++) {
-        const int j = sum - i;
-        if (j < i || j > 5) continue;
-        lin_add_f2<F>(acc, prod + 3 * vw_pair_index<C>(i, j) * L, im, w == 1, i != j ? 2 : 1);
-      }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      const bool wrap = i > k;
+      const int j = wrap ? k + 6 - i : k - i;
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      lin_add_f2<F>(acc, prod + 3 * vw_pair_index<C>(lo, hi) * L, im, wrap, 1);
     }
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -546,6 +549,111 @@ KZGX_TW void vw_inv(uint32_t dst_o, uint32_t a_o) {
   __syncthreads();
 }
 
+// dst = a^-1 by the whole wave (replaces the one-lane tower inverse, ~140 us
+// on BN254 -- a hundred dependent Fp products in one lane): with conj the
+// p^6-Frobenius (odd coefficients negated),
+//   a^-1 = conj(a) / N,   N = a conj(a) = n0 + n1 v + n2 v^2 in Fp6 (v = w^2),
+//   N^-1 = (A + B v + C v^2) / F,  A = n0^2 - xi n1 n2,  B = xi n2^2 - n0 n1,
+//   C = n1^2 - n0 n2,  F = n0 A + xi (n2 B + n1 C) in Fp2,
+//   F^-1 = conj2(F) / (F.re^2 + F.im^2), one Fp inversion (wave-uniform).
+// Rounds of Karatsuba parts, one per lane, with lazy folds; ta, tb are two
+// free slots (ta = conj(a); tb = N, then A, B, C in its odd positions, then
+// N^-1 in its even positions).
+template <class C>
+KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t tb_o, uint32_t prod_o) {
+  using F = typename C::Fp29;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  uint32_t* prod = vw_smem + prod_o;
+  uint32_t* tb = vw_smem + tb_o;
+  uint32_t* sc = prod + 64 * L;  // scratch past the parts: F (2L), t (L), F^-1 (2L)
+  const int lane = threadIdx.x;
+  vw_conj<C>(ta_o, a_o);
+  vw_mul<C>(tb_o, a_o, ta_o, prod_o);
+  // (n0, n1, n2) = tb[0], tb[2], tb[4]
+  // round A: n0^2, n1 n2, n2^2, n0 n1, n1^2, n0 n2
+  if (lane < 18) {
+    const int pr = lane / 3;
+    const int x = pr == 0 ? 0 : pr == 1 ? 2 : pr == 2 ? 4 : pr == 3 ? 0 : pr == 4 ? 2 : 0;
+    const int y = pr == 0 ? 0 : pr == 1 ? 4 : pr == 2 ? 4 : pr == 3 ? 2 : pr == 4 ? 2 : 4;
+    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + y * E2), lane % 3));
+  }
+  __syncthreads();
+  if (lane < 6) {  // A, B, C -> tb[1], tb[3], tb[5]
+    const int c = lane >> 1, im = lane & 1;
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    if (c == 0) {
+      lin_add_f2<F>(acc, prod + 0 * 3 * L, im, false, 1);
+      lin_add_f2<F>(acc, prod + 1 * 3 * L, im, true, -1);
+    } else if (c == 1) {
+      lin_add_f2<F>(acc, prod + 2 * 3 * L, im, true, 1);
+      lin_add_f2<F>(acc, prod + 3 * 3 * L, im, false, -1);
+    } else {
+      lin_add_f2<F>(acc, prod + 4 * 3 * L, im, false, 1);
+      lin_add_f2<F>(acc, prod + 5 * 3 * L, im, false, -1);
+    }
+    vw_st<C>(tb + (2 * c + 1) * E2 + im * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  // round B: n0 A, n2 B, n1 C -> F = n0 A + xi (n2 B + n1 C)
+  if (lane < 9) {
+    const int pr = lane / 3;
+    const int x = pr == 0 ? 0 : pr == 1 ? 4 : 2;
+    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + (2 * pr + 1) * E2), lane % 3));
+  }
+  __syncthreads();
+  if (lane < 2) {
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add_f2<F>(acc, prod, lane, false, 1);
+    lin_add_f2<F>(acc, prod + 3 * L, lane, true, 1);
+    lin_add_f2<F>(acc, prod + 6 * L, lane, true, 1);
+    vw_st<C>(sc + lane * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  // round C: t = F.re^2 + F.im^2
+  if (lane < 2) {
+    const F29<F> v = vw_ld<C>(sc + lane * L);
+    vw_st<C>(prod + lane * L, f29_mul<F>(v, v));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    LinAcc<F> acc;
+    lin_init<F>(acc);
+    lin_add<F>(acc, prod, 1);
+    lin_add<F>(acc, prod + L, 1);
+    vw_st<C>(sc + 2 * L, lin_fin<F>(acc));
+  }
+  __syncthreads();
+  // t^-1 by the whole wave (lane 0's value, binary GCD on the scalar ALU)
+  const F29<F> ti = f29_inv_uniform<F, C::Fp::N>(vw_ld<C>(sc + 2 * L), C::Fp::P);
+  // F^-1 = (F.re t^-1, -F.im t^-1)
+  if (lane < 2) {
+    const F29<F> v = f29_mul<F>(vw_ld<C>(sc + lane * L), ti);
+    vw_st<C>(sc + 3 * L + lane * L, lane ? fp_neg<F>(v) : v);
+  }
+  __syncthreads();
+  // round E: A F^-1, B F^-1, C F^-1 -> tb = [A', 0, B', 0, C', 0]
+  if (lane < 9) {
+    const int pr = lane / 3;
+    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + (2 * pr + 1) * E2), vw_ld2<C>(sc + 3 * L), lane % 3));
+  }
+  __syncthreads();
+  if (lane < 12) {
+    const int k = lane >> 1, im = lane & 1;
+    F29<F> v = f29_zero<F>();
+    if (!(k & 1)) {
+      LinAcc<F> acc;
+      lin_init<F>(acc);
+      lin_add_f2<F>(acc, prod + (k >> 1) * 3 * L, im, false, 1);
+      v = lin_fin<F>(acc);
+    }
+    vw_st<C>(tb + k * E2 + im * L, v);
+  }
+  __syncthreads();
+  vw_mul<C>(dst_o, ta_o, tb_o, prod_o);
+}
+
 // final exponentiation as a small program over Fp12 slots (the chains of
 // final_exp), run by one loop so that every wave-wide op is inlined once and
 // no call (with its register save / restore through scratch) sits between
@@ -580,7 +688,7 @@ KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
       case VW_CSQR: vw_cyclo_sqr<C>(d, a, prod); break;
       case VW_CONJ: vw_conj<C>(d, a); break;
       case VW_FROB: vw_frob<C>(d, a, prod); break;
-      case VW_INV: vw_inv<C>(d, a); break;
+      case VW_INV: vw_inv_wave<C>(d, a, slots + 7 * E, slots + 8 * E, prod); break;
       default: {  // d = a^e (cyclotomic a, top bit of e set), d != a
         uint64_t e0 = op[3], e1 = 0;
         int bits = 32 - __builtin_clz((uint32_t)op[3] | 1u);
@@ -1116,6 +1224,61 @@ __global__ __launch_bounds__(64) void k_pair2_wave(const uint32_t* __restrict__ 
   }
   __syncthreads();
   vw_pair_tail<C>(vlines, ok);
+}
+
+// Debug / measurement (kzgx_debug_vw_bench, not in kzg_gpu.h): the latency
+// of one wave-wide Fp12 op, iterated `iters` times on arbitrary values < m
+// in LDS: 0 cyclotomic squaring, 1 dense product, 2 squaring, 3 line
+// product, 4 Frobenius, 5 one-lane inverse, 6 wave inverse.  out[0] = wall-clock ticks
+// (100 MHz), out[1] = core clocks (s_memtime).
+template <class C>
+__global__ __launch_bounds__(64) void k_vw_bench(int op, uint32_t iters, uint64_t* __restrict__ out) {
+  using V = VWave<C>;
+  constexpr int L = V::L;
+  const uint32_t lane = threadIdx.x;
+  constexpr uint32_t s0 = V::O_SLOT, s1 = V::O_SLOT + V::E12;
+  // arbitrary values below m: pseudo-random low limbs, a small top limb
+  for (uint32_t w = lane; w < (uint32_t)V::O_PROD; w += 64) {
+    const uint32_t h = (w + 1) * 2654435761u;
+    vw_smem[w] = (w % L == L - 1) ? (h >> 24) : (h >> 3);
+  }
+  __syncthreads();
+  const uint64_t w0 = wall_clock64(), c0 = clock64();
+#pragma unroll 1
+  for (uint32_t it = 0; it < iters; it++) {
+    switch (op) {
+      case 0: vw_cyclo_sqr<C>(s0, s0, V::O_PROD); break;
+      case 1: vw_mul<C>(s0, s0, s1, V::O_PROD); break;
+      case 2: vw_sqr<C>(s0, s0, V::O_PROD); break;
+      case 3: vw_mul_line<C>(s0, V::O_LINES, V::O_PROD); break;
+      case 4: vw_frob<C>(s0, s0, V::O_PROD); break;
+      case 5: vw_inv<C>(s1, s0); break;
+      default: vw_inv_wave<C>(s1, s0, s1 + V::E12, s1 + 2 * V::E12, V::O_PROD); break;
+    }
+  }
+  const uint64_t w1 = wall_clock64(), c1 = clock64();
+  if (lane == 0) {
+    out[0] = w1 - w0;
+    out[1] = c1 - c0;
+  }
+}
+
+int vw_bench(int curve, int op, uint32_t iters, double* ns_per_op, double* clk_per_op, hipStream_t st) {
+  uint64_t* d = nullptr;
+  KZGX_TRY_HIP(hipMalloc((void**)&d, 16));
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_vw_bench<BN254G1>, dim3(1), dim3(64), VWave<BN254G1>::WORDS * 4, st, op, iters, d);
+  else
+    hipLaunchKernelGGL(k_vw_bench<BLS12381G1>, dim3(1), dim3(64), VWave<BLS12381G1>::WORDS * 4, st, op, iters, d);
+  uint64_t h[2] = {0, 0};
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e);
+  *ns_per_op = 10.0 * (double)h[0] / iters;
+  *clk_per_op = (double)h[1] / iters;
+  return KZGX_OK;
 }
 
 // wave path: [y]G table | line tables | Q flags, in one device buffer

@@ -1,30 +1,66 @@
-"""Single large MSMs on the table-less Pippenger path (host buffers, medians
-of 5): the per-rank partial of the sharded degree-2^20 commit (2^19 points
-on 2 ranks) and the benchmark-common sizes.  KZGX_* knobs apply."""
+"""Single large MSMs on the table-less path (no default / fixed table):
+device-resident scalars, HIP events on the call's stream, median of 7, every
+result checked against [P(tau)]G1.  Sizes: the 8-way shard of the sharded
+degree-2^20 commit (131 073 points on an SRS of that size, as each rank
+holds), 2^17, the 2-way shard (2^19 + 1) and the whole degree-2^20 commit
+(2^20 + 1).  From 2^16 points the wide-window path runs (msm.hip msm_big:
+c = 14 / 15 / 16 by SRS size); KZGX_BIG_MIN=0 restores the round-4 chunked
+c = 12 Pippenger for A/B.  Prints one JSON line per size."""
+import json
 import os
 import sys
-import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kzg-commitments_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import torch  # noqa: E402,F401
 import kzgx  # noqa: E402
 import kzg_ref as K  # noqa: E402
+import corc  # noqa: E402  (checker only: Horner of P at tau)
 
 C = K.BN254
-ctx = kzgx.Context("BN254")
-ctx.set_default_table(0)
-ctx.gen_srs(K.default_tau(C), (1 << 20) + 1)
+tau = K.default_tau(C)
 rng = np.random.default_rng(5)
-P = rng.integers(0, 2**63, size=((1 << 20) + 1, 4), dtype=np.uint64)
+NMAX = (1 << 20) + 1
+P = rng.integers(0, 2**63, size=(NMAX, 4), dtype=np.uint64)
 P[:, 3] &= np.uint64((1 << 59) - 1)
-for n in (1 << 14, 1 << 17, (1 << 19) + 1, (1 << 20) + 1):
-    ctx.msm(P[:n])
-    ts = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        ctx.msm(P[:n])
-        ts.append(time.perf_counter() - t0)
-    print("pippenger n=%8d %.3f ms" % (n, 1e3 * float(np.median(ts))), flush=True)
+corc.build()
+
+
+def run(srs_n, n):
+    ctx = kzgx.Context("BN254")
+    try:
+        ctx.set_default_table(0)
+        ctx.gen_srs(tau, srs_n)
+        d_s = torch.from_numpy(P[:n].copy().view(np.int64)).cuda()
+        d_o = torch.zeros((8,), dtype=torch.int64, device="cuda")
+        d_i = torch.zeros((1,), dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        ts = []
+        for rep in range(9):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            ctx.msm_batch_device(d_s.data_ptr(), n, 1, n, d_o.data_ptr(), d_i.data_ptr(), st.cuda_stream)
+            b.record(st)
+            b.synchronize()
+            if rep >= 2:
+                ts.append(a.elapsed_time(b))
+        out = d_o.cpu().numpy().view(np.uint64)
+        inf = bool(d_i.cpu().item())
+        got = None if inf else (sum(int(out[j]) << (64 * j) for j in range(4)),
+                                sum(int(out[4 + j]) << (64 * j) for j in range(4)))
+        exp = K.scalar_mul(C, (C.gx, C.gy), corc.poly_eval("BN254", P[:n], tau))
+        rec = {"srs_points": srs_n, "n": n, "median_ms": float(np.median(ts)), "min_ms": float(min(ts)),
+               "per_s": 1e3 / float(np.median(ts)), "checked": got == exp,
+               "path": "chunked c=12" if os.environ.get("KZGX_BIG_MIN") == "0" else "wide-window"}
+        print(json.dumps(rec), flush=True)
+        assert got == exp
+    finally:
+        ctx.close()
+
+
+for srs_n, n in ((131073, 131073), ((1 << 17), (1 << 17)), ((1 << 19) + 1, (1 << 19) + 1), (NMAX, NMAX)):
+    run(srs_n, n)

@@ -7,7 +7,7 @@
 # call (no GPU work after a fault, abort or timeout).  Outputs land in
 # gpurun_out/TAG/.  Steps:
 #   micro[:BIN]       scripts/mb/BIN (mixed-add variants; default: all)
-#   tests[:K]         pytest -m gpu (optionally -k K)
+#   tests[:K]         pytest -m gpu (optionally -k K, commas -> spaces)
 #   smoke             __graft_entry__.smoke()
 #   bench[:ARGS]      python bench.py ARGS (commas -> spaces)
 #   prof[:ARGS]       rocprofv3 --kernel-trace --stats around bench.py ARGS
@@ -39,7 +39,7 @@ for st in "$@"; do
       ;;
     tests)
       k=()
-      [[ -n "$arg" ]] && k=(-k "$arg")
+      [[ -n "$arg" ]] && k=(-k "${arg//,/ }")
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$OUT/tests_$n.log" 2>&1 || { tail -30 "$OUT/tests_$n.log"; exit 1; }
       tail -3 "$OUT/tests_$n.log"

@@ -9,7 +9,7 @@
 //   nt_builtin: __builtin_nontemporal_load (the compiler's streaming form)
 //   asm_<bits>: global_load_dwordx4 with the gfx950 cache-policy bits
 //               sc0 / sc1 / nt in every combination
-//   buffer    : raw buffer loads (aux 0, and the slc / glc bits)
+//   buffer    : raw buffer loads (aux 0; aux 2 = nt, aux 1 = sc0 on gfx950)
 // Each launch prints its algorithmic bytes and time; rocprofv3 --pmc
 // TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum gives
 // the DRAM request sizes per dispatch (scripts/gpu.sh profbin / pmc steps).
@@ -130,8 +130,8 @@ int main(int argc, char** argv) {
   run<P_SC1_NT>("asm_sc1_nt", tab, bytes, gathers, sink);
   run<P_SC0_SC1_NT>("asm_sc0_sc1_nt", tab, bytes, gathers, sink);
   run<P_BUF>("buffer", tab, bytes, gathers, sink);
-  run<P_BUF_SLC>("buffer_slc", tab, bytes, gathers, sink);
-  run<P_BUF_GLC>("buffer_glc", tab, bytes, gathers, sink);
+  run<P_BUF_SLC>("buffer_nt", tab, bytes, gathers, sink);
+  run<P_BUF_GLC>("buffer_sc0", tab, bytes, gathers, sink);
   run<P_DEFAULT>("default_again", tab, bytes, gathers, sink);
   CHECK(hipFree(tab));
   CHECK(hipFree(sink));

@@ -126,10 +126,10 @@ def test_sparse_and_small_scalars(name, C):
 
 # ---- the wide-window single-MSM path (msm.hip msm_big, round 5) ----------------
 # An SRS of >= 2^16 points gets a wide-window table at setup: c = 14 below
-# 2^17 points, 15 below 2^18, 16 from there; single MSMs of >= 2^16 points
+# 2^18 points, 16 from there; single MSMs of >= 2^16 points
 # take it (global counting sort, LDS histograms of 2^(c-1) buckets, the
 # batched accumulation / merges, latency.hip's bucket reduction).
-BIG = [(65536 + 7, 14), (131072 + 3, 15), (262144 + 1, 16)]
+BIG = [(65536 + 7, 14), (131072 + 3, 14), (262144 + 1, 16)]
 
 
 @pytest.mark.parametrize("name,C", CURVES)
