@@ -71,5 +71,11 @@ int vw_bench(int curve, int op, uint32_t iters, double* ns_per_op, double* clk_p
 size_t big_reduce_rt_bytes(int curve, uint32_t nb);
 int big_reduce(int curve, const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
                uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
+// the same from bucket-aligned segment partials (msm.hip k_big2_*): bucket k
+// owns part[seg_off[k] .. seg_off[k + 1]); s_ub bounds seg_off[nb]; *d_flag:
+// some bucket has more than 64 partials (pre-sum passes run); part is
+// overwritten
+int big_reduce_seg(int curve, const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
+                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 
 }  // namespace kzgx

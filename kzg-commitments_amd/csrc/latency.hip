@@ -1,7 +1,6 @@
-// Lone-wave kernels outside the verify path, compiled with the latency-first
-// Fp product (field29.hpp f29_mul_lat, KZGX_FIELD_LATENCY): work that is one
-// dependent chain on one wave, where a product's dependency depth -- not its
-// instruction count -- is the cost.
+// Lone-wave kernels outside the verify path: work that is one dependent
+// chain on one wave (the sharded commitment's fold, the bucket reduction of
+// the wide-window Pippenger MSM).
 //
 // k_g1_fold_packed: the exact fold of the sharded commitment (BASELINE
 // configs[4], python/kzgx_dist.py): the N ranks' partial points, all-gathered
@@ -13,7 +12,17 @@
 // one-lane k_g1_sum ("What's weak" 4).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
+// The product form: the chained (throughput) form by default -- measured
+// faster here than the latency-first f29_mul_lat (2^20 + 1 points 2.579 vs
+// 2.603 ms, 131 073: 0.691 vs 0.724 ms, profiles/r05_big_msm_*): an XYZZ
+// addition has enough independent products that one lane's chain of them
+// is issue-bound either way.  KZGX_LATENCY_LAT selects f29_mul_lat (A/B).
+#ifdef KZGX_LATENCY_LAT
 #define KZGX_FIELD_LATENCY
+#endif
+#include "coop.hpp"
 #include "curve.hpp"
 #include "kzgx_internal.hpp"
 #include "kzgx_setup.hpp"
@@ -141,12 +150,29 @@ KZGX_DEV Xyzz<C> wave_total(Xyzz<C> U, uint32_t n) {
   return U;
 }
 
+// workgroups g < NG: V_g = sum_l R_l + J sum_l l T_l over the group's 256
+// pairs.  Workgroups NG + g: T'_g = 512 T_g (J BIG_F1 = 512), the group
+// total scaled for the second level, on its own CU so that its 9 doublings
+// run beside V_g's chain instead of after it (k_lat_fold2 then needs none).
 template <class C>
-__global__ __launch_bounds__(BIG_F1) void k_lat_fold1(const uint32_t* __restrict__ rt, uint32_t* __restrict__ vt) {
+__global__ __launch_bounds__(BIG_F1) void k_lat_fold1(const uint32_t* __restrict__ rt, uint32_t NG,
+                                                      uint32_t* __restrict__ vt) {
   constexpr int XW = xyzz_words<C>();
   constexpr uint32_t NW = BIG_F1 / 64;
+  static_assert(NW == 4, "k_lat_fold1: four waves");
   __shared__ uint32_t lds[NW * XW];
   const uint32_t l = threadIdx.x, lane = l & 63, wv = l >> 6;
+  if (blockIdx.x >= NG) {
+    const uint32_t g = blockIdx.x - NG;
+    Xyzz<C> T = wave_total<C>(xyzz_load<C>(rt + ((size_t)g * BIG_F1 + l) * 2 * XW + XW), 64);
+    if (lane == 0) xyzz_store<C>(lds + wv * XW, T);
+    __syncthreads();
+    if (l != 0) return;
+    T = xyzz_add_impl<C>(xyzz_add_impl<C>(T, xyzz_load<C>(lds + XW)),
+                         xyzz_add_impl<C>(xyzz_load<C>(lds + 2 * XW), xyzz_load<C>(lds + 3 * XW)));
+    xyzz_store<C>(vt + (size_t)g * 2 * XW + XW, xyzz_dbl_pow2<C>(T, BIG_RED_J * BIG_F1));
+    return;
+  }
   const uint32_t* src = rt + ((size_t)blockIdx.x * BIG_F1 + l) * 2 * XW;
   const Xyzz<C> R = xyzz_load<C>(src);
   Xyzz<C> S = wave_suffix<C>(xyzz_load<C>(src + XW), lane, 64);
@@ -154,18 +180,18 @@ __global__ __launch_bounds__(BIG_F1) void k_lat_fold1(const uint32_t* __restrict
   __syncthreads();
 #pragma unroll 1
   for (uint32_t w = wv + 1; w < NW; w++) S = xyzz_add_impl<C>(S, xyzz_load<C>(lds + w * XW));
-  const Xyzz<C> Tg = S;  // thread 0: the group total
   __syncthreads();  // lds is reused below
   Xyzz<C> U = R;
   if (l > 0) U = xyzz_add_impl<C>(U, xyzz_dbl_pow2<C>(S, BIG_RED_J));
   U = wave_total<C>(U, 64);
   if (lane == 0) xyzz_store<C>(lds + wv * XW, U);
   __syncthreads();
+  // (U0 + U1) + (U2 + U3): waves 0 and 2 in parallel, then thread 0
+  if (l == 128) xyzz_store<C>(lds + 2 * XW, xyzz_add_impl<C>(U, xyzz_load<C>(lds + 3 * XW)));
+  if (l == 0) U = xyzz_add_impl<C>(U, xyzz_load<C>(lds + XW));
+  __syncthreads();
   if (l != 0) return;
-#pragma unroll 1
-  for (uint32_t w = 1; w < NW; w++) U = xyzz_add_impl<C>(U, xyzz_load<C>(lds + w * XW));
-  xyzz_store<C>(vt + (size_t)blockIdx.x * 2 * XW, U);
-  xyzz_store<C>(vt + (size_t)blockIdx.x * 2 * XW + XW, Tg);
+  xyzz_store<C>(vt + (size_t)blockIdx.x * 2 * XW, xyzz_add_impl<C>(U, xyzz_load<C>(lds + 2 * XW)));
 }
 
 template <class C>
@@ -176,10 +202,10 @@ __global__ __launch_bounds__(64) void k_lat_fold2(const uint32_t* __restrict__ v
   Xyzz<C> V = xyzz_inf<C>(), S = xyzz_inf<C>();
   if (lane < NG) {
     V = xyzz_load<C>(vt + (size_t)lane * 2 * XW);
-    S = xyzz_load<C>(vt + (size_t)lane * 2 * XW + XW);
+    S = xyzz_load<C>(vt + (size_t)lane * 2 * XW + XW);  // already 512 T_g
   }
   S = wave_suffix<C>(S, lane, NG);
-  if (lane > 0 && lane < NG) V = xyzz_add_impl<C>(V, xyzz_dbl_pow2<C>(S, BIG_RED_J * BIG_F1));
+  if (lane > 0 && lane < NG) V = xyzz_add_impl<C>(V, S);
   V = wave_total<C>(V, NG);
   Xyzz<C> v;
 #pragma unroll
@@ -199,7 +225,115 @@ __global__ __launch_bounds__(64) void k_lat_fold2(const uint32_t* __restrict__ v
 size_t big_reduce_rt_bytes(int curve, uint32_t nb) {
   const size_t xb = 4 * (curve == KZGX_CURVE_BN254 ? xyzz_words<BN254G1>() : xyzz_words<BLS12381G1>());
   const size_t T1 = nb / BIG_RED_J;
-  return (T1 + T1 / BIG_F1) * 2 * xb;
+  return (T1 + T1 / 16 + 4) * 2 * xb;  // the pairs, then the fold levels' outputs
+}
+
+// ---- group-cooperative fold levels (coop.hpp): the top of the reduction ----
+// A level reduces N (R_t, T_t) pairs, V = sum_t R_t + 2^JLOG t T_t, 32 pairs
+// per 256-thread workgroup (one 8-lane group per pair):
+//   workgroups b < NGo:  V_b = sum_l R_l + 2^JLOG l T_l over its pairs
+//                        (suffix sums S_l by group shuffles + the higher
+//                        waves' totals; sum_l l T_l = sum_{l >= 1} S_l)
+//   workgroups NGo + b:  T'_b = 2^(5 + JLOG) sum_l T_l, beside V_b's chain,
+// so the next level sees pairs (V_b, T'_b) with JLOG = 0.  Every point op is
+// one cooperative addition / doubling (~1/3 of a lone lane's latency).
+template <class C, int JLOG>
+__global__ __launch_bounds__(256) void k_coop_fold(const uint32_t* __restrict__ in, uint32_t N, uint32_t NGo,
+                                                   uint32_t* __restrict__ out) {
+  using F = typename C::Fp29;
+  constexpr int XW = xyzz_words<C>(), L = F::L;
+  __shared__ uint32_t sc[32 * COOP_SLOTS * L];
+  __shared__ uint32_t wt[4 * XW];
+  const uint32_t t = threadIdx.x, wv = t >> 6, g = t >> 3, gw = (t & 63) >> 3;
+  const int j = (int)(t & 7);
+  uint32_t* my = sc + g * COOP_SLOTS * L;
+  const bool tpath = blockIdx.x >= NGo;
+  const uint32_t b = tpath ? blockIdx.x - NGo : blockIdx.x;
+  const uint32_t idx = b * 32 + g;
+  const uint32_t* src = in + (size_t)idx * 2 * XW;
+  if (tpath) {
+    Xyzz<C> T = idx < N ? xyzz_load<C>(src + XW) : xyzz_inf<C>();
+#pragma unroll 1
+    for (int o = 4; o >= 1; o >>= 1) T = coop_add<C>(T, xyzz_shfl_down_w<C>(T, 8 * o), my, j);
+    if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, T);
+    __syncthreads();
+    if (t >= 16) return;
+    // groups 0 and 1 of wave 0: (wt0 + wt1), (wt2 + wt3); then group 0 adds
+    T = coop_add<C>(xyzz_load<C>(wt + (2 * g) * XW), xyzz_load<C>(wt + (2 * g + 1) * XW), my, j);
+    T = coop_add<C>(T, xyzz_shfl_down_w<C>(T, 8), my, j);
+#pragma unroll 1
+    for (int d = 0; d < 5 + JLOG; d++) T = coop_dbl<C>(T, my, j);
+    if (t == 0) xyzz_store<C>(out + (size_t)b * 2 * XW + XW, T);
+    return;
+  }
+  const Xyzz<C> R = idx < N ? xyzz_load<C>(src) : xyzz_inf<C>();
+  Xyzz<C> S = idx < N ? xyzz_load<C>(src + XW) : xyzz_inf<C>();
+#pragma unroll 1
+  for (uint32_t o = 1; o < 8; o <<= 1) {
+    const Xyzz<C> x = xyzz_shfl_down_w<C>(S, (int)(8 * o));
+    if (gw + o < 8) S = coop_add<C>(S, x, my, j);
+  }
+  if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, S);
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t w = wv + 1; w < 4; w++) S = coop_add<C>(S, xyzz_load<C>(wt + w * XW), my, j);
+  __syncthreads();  // wt is reused below
+  Xyzz<C> U = R;
+  if (g > 0) {
+#pragma unroll 1
+    for (int d = 0; d < JLOG; d++) S = coop_dbl<C>(S, my, j);
+    U = coop_add<C>(U, S, my, j);
+  }
+#pragma unroll 1
+  for (int o = 4; o >= 1; o >>= 1) U = coop_add<C>(U, xyzz_shfl_down_w<C>(U, 8 * o), my, j);
+  if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, U);
+  __syncthreads();
+  if (t < 8 || (t >= 128 && t < 136)) {  // group 0 of waves 0 and 2
+    const Xyzz<C> o = xyzz_load<C>(wt + (wv + 1) * XW);
+    U = coop_add<C>(U, o, my, j);
+    if (t == 128) xyzz_store<C>(wt + 2 * XW, U);
+  }
+  __syncthreads();
+  if (t >= 8) return;
+  U = coop_add<C>(U, xyzz_load<C>(wt + 2 * XW), my, j);
+  if (t == 0) xyzz_store<C>(out + (size_t)b * 2 * XW, U);
+}
+
+// the last level's V (pair 0's R slot) -> canonical affine, by one wave
+template <class C>
+__global__ __launch_bounds__(64) void k_coop_finish(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                    uint32_t* __restrict__ out_inf) {
+  const Xyzz<C> V = xyzz_load<C>(in);
+  Affine<C> a;
+  const bool fin = xyzz_to_affine_impl<C, true>(V, a);
+  if (threadIdx.x != 0) return;
+  affine_to_canonical<C>(out, a, fin);
+  *out_inf = fin ? 0u : 1u;
+}
+
+// rt holds T1 pairs (R_t, T_t) with J = 2: coop levels down to one point
+template <class C>
+static int coop_levels(uint32_t* d_rt, uint32_t T1, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  constexpr int XW = xyzz_words<C>();
+  uint32_t* in = d_rt;
+  uint32_t* nxt = d_rt + (size_t)T1 * 2 * XW;
+  uint32_t N = T1;
+  bool first = true;
+  for (;;) {
+    const uint32_t NG = (N + 31) / 32;
+    if (first)
+      hipLaunchKernelGGL((k_coop_fold<C, 1>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, nxt);
+    else
+      hipLaunchKernelGGL((k_coop_fold<C, 0>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, nxt);
+    first = false;
+    in = nxt;
+    nxt += (size_t)NG * 2 * XW;
+    N = NG;
+    if (N == 1) break;
+  }
+  hipLaunchKernelGGL(k_coop_finish<C>, dim3(1), dim3(64), 0, st, in, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
 }
 
 template <class C>
@@ -209,10 +343,123 @@ static int big_reduce_impl(const uint32_t* d_offsets, uint32_t nb, const uint32_
   if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb in [512, 2^15]
   uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
   hipLaunchKernelGGL(k_lat_bucket_sums<C>, dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum, d_rt);
-  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(NG), dim3(BIG_F1), 0, st, d_rt, vt);
+  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
   hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
+}
+
+// ---- bucket-aligned segments (msm.hip k_big2_*): partials -> (R_t, T_t) ----
+KZGX_DEV uint32_t lat_seg_bucket(const uint32_t* __restrict__ seg_off, uint32_t nb, uint32_t j) {
+  uint32_t lo = 0, hi = nb;  // seg_off[lo] <= j < seg_off[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+// stride of a bucket's live partials after the pre-sum passes: the smallest
+// 8^p with ceil(s / 8^p) <= BIG_MAXSEG
+constexpr uint32_t LAT_MAXSEG = 64;  // msm.hip BIG_MAXSEG
+KZGX_DEV uint32_t lat_seg_stride(uint32_t s) {
+  uint32_t st = 1;
+  while ((s + st - 1) / st > LAT_MAXSEG) st *= 8;
+  return st;
+}
+
+// pre-sum pass p (1, 2, ...) for buckets with more than LAT_MAXSEG segment
+// partials (skewed scalars): the partials at stride 8^(p-1) are summed 8 to
+// 1 into the positions that are multiples of 8^p.  No-op unless *flag.
+template <class C>
+__global__ __launch_bounds__(256) void k_lat_long(const uint32_t* __restrict__ seg_off, uint32_t nb, uint32_t sp,
+                                                  const uint32_t* __restrict__ flag, uint32_t* __restrict__ part) {
+  constexpr int XW = xyzz_words<C>();
+  if (!*flag) return;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= seg_off[nb]) return;
+  const uint32_t k = lat_seg_bucket(seg_off, nb, j);
+  const uint32_t s = seg_off[k + 1] - seg_off[k];
+  if ((s + sp - 1) / sp <= LAT_MAXSEG) return;
+  const uint32_t i = j - seg_off[k];
+  if (i % (8 * sp)) return;
+  uint32_t* base = part + (size_t)seg_off[k] * XW;
+  Xyzz<C> acc = xyzz_load<C>(base + (size_t)i * XW);
+  for (uint32_t m = 1; m < 8 && i + m * sp < s; m++) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(base + (size_t)(i + m * sp) * XW));
+  xyzz_store<C>(base + (size_t)i * XW, acc);
+}
+
+template <class C>
+KZGX_DEV Xyzz<C> xyzz_shfl_xor_w(const Xyzz<C>& p, int m) {
+  Xyzz<C> o;
+#pragma unroll
+  for (int k = 0; k < C::Fp29::L; k++) {
+    o.X.v[k] = __shfl_xor(p.X.v[k], m, 64);
+    o.Y.v[k] = __shfl_xor(p.Y.v[k], m, 64);
+    o.ZZ.v[k] = __shfl_xor(p.ZZ.v[k], m, 64);
+    o.ZZZ.v[k] = __shfl_xor(p.ZZZ.v[k], m, 64);
+  }
+  return o;
+}
+
+// G lanes per bucket, 2 G per pair t: B_k = the sum of bucket k's partials
+// (lane-strided, then a G-lane shuffle tree), T_t = B_2t + B_2t+1 (lane 0
+// stores), R_t = T_t + B_2t+1 (lane G stores)
+template <class C, uint32_t G>
+__global__ __launch_bounds__(256) void k_lat_seg_sums(const uint32_t* __restrict__ seg_off, uint32_t nb,
+                                                      const uint32_t* __restrict__ part, uint32_t* __restrict__ rt) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = gid / (2 * G), q = gid % (2 * G);
+  if (t >= nb / 2) return;  // whole pair groups
+  const uint32_t k = 2 * t + q / G, sub = q % G;
+  const uint32_t s0 = seg_off[k], s = seg_off[k + 1] - s0;
+  const uint32_t sp = lat_seg_stride(s), c = (s + sp - 1) / sp;
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t i = sub; i < c; i += G) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(part + (size_t)(s0 + i * sp) * XW));
+#pragma unroll 1
+  for (uint32_t m = 1; m < G; m <<= 1) acc = xyzz_add_impl<C>(acc, xyzz_shfl_xor_w<C>(acc, (int)m));
+  const Xyzz<C> T = xyzz_add_impl<C>(acc, xyzz_shfl_xor_w<C>(acc, (int)G));
+  if (q == 0) xyzz_store<C>(rt + (size_t)t * 2 * XW + XW, T);
+  if (q == G) xyzz_store<C>(rt + (size_t)t * 2 * XW, xyzz_add_impl<C>(T, acc));
+}
+
+template <class C>
+static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
+                               const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf,
+                               hipStream_t st) {
+  const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
+  if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;
+  uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
+  // pre-sum passes: as many as the largest possible bucket (s_ub partials)
+  // could need; each exits at once unless some bucket has > LAT_MAXSEG
+  for (uint64_t sp = 1; (s_ub + sp - 1) / sp > LAT_MAXSEG; sp *= 8)
+    hipLaunchKernelGGL(k_lat_long<C>, dim3((s_ub + 255) / 256), dim3(256), 0, st, d_seg_off, nb, (uint32_t)sp, d_flag,
+                       d_part);
+  // lanes per bucket: 8 when buckets hold more than ~8 partials on average
+  if (s_ub / nb > 8)
+    hipLaunchKernelGGL((k_lat_seg_sums<C, 8>), dim3((nb * 8 + 255) / 256), dim3(256), 0, st, d_seg_off, nb, d_part,
+                       d_rt);
+  else
+    hipLaunchKernelGGL((k_lat_seg_sums<C, 4>), dim3((nb * 4 + 255) / 256), dim3(256), 0, st, d_seg_off, nb, d_part,
+                       d_rt);
+  // the fold: group-cooperative levels (KZGX_BIG_LONEFOLD: the lone-lane
+  // k_lat_fold1 / k_lat_fold2, A/B)
+  static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
+  if (!lone) return coop_levels<C>(d_rt, T1, d_out, d_out_inf, st);
+  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
+  hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int big_reduce_seg(int curve, const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
+                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  return curve == KZGX_CURVE_BN254
+             ? big_reduce_seg_impl<BN254G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st)
+             : big_reduce_seg_impl<BLS12381G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st);
 }
 
 int big_reduce(int curve, const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,

@@ -776,6 +776,339 @@ __global__ __launch_bounds__(BIG_TPB) void k_big_scatter(const uint32_t* __restr
   }
 }
 
+// ---- two-pass sort and bucket-aligned segments (round 5) ----
+// With 2^(c-1) = 8192..32768 buckets, a per-block bucket histogram is as
+// large as the block's digits, so the one-pass sort above spends most of its
+// time on its own count rows (the 2^20 + 1 MSM: 461 us of sort for 1.3 ms of
+// accumulation, profiles/r05_big_msm_*).  Instead:
+//   pass 1: BIG_NC = 1024 coarse bins (the high bits of the bucket): per-block
+//           LDS histograms of 1024 counters, a per-bin scan over the blocks
+//           (one workgroup per bin), a 1024-entry scan, and a scatter of
+//           packed entries (table index | fine bits << 26 | sign << 31) in
+//           runs of ~34 per (block, bin);
+//   pass 2: one workgroup per coarse bin ranks its ~17k entries by the fine
+//           bits in LDS and writes them in bucket order (bucket offsets too),
+//           and cuts every bucket into ceil(len / K) accumulation segments
+//           that never cross a bucket, so no merge of crossing partials is
+//           needed: the reduction sums each bucket's few segment partials.
+// Used when the table index fits 26 bits (W n_rows < 2^26: SRSs up to
+// ~3.9M points at c = 16); larger SRSs keep the one-pass sort and merge.
+constexpr uint32_t BIG_NC = 1024;
+constexpr uint32_t BIG_IDX_BITS = 26;
+constexpr uint32_t BIG_MAXSEG = 64;  // segment partials per bucket the reduction sums directly
+
+template <int CB>
+struct BigFine {
+  static constexpr uint32_t NF = Win<CB>::NB / BIG_NC;  // buckets per coarse bin
+  static constexpr int FB = CB - 1 - 10;
+  static_assert(NF >= 2 && NF <= 32 && (1u << FB) == NF, "c = 12..16");
+};
+
+template <int CB>
+__global__ __launch_bounds__(BIG_TPB) void k_big2_count(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                        const uint8_t* __restrict__ inf, uint32_t per, uint32_t nblk,
+                                                        uint32_t* __restrict__ counts_t) {
+  constexpr int W = Win<CB>::W;
+  constexpr int FB = BigFine<CB>::FB;
+  __shared__ uint32_t hist[BIG_NC];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+#pragma unroll 1
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += BIG_TPB) {
+    if (inf[i]) continue;
+    uint32_t s[8];
+    load_scalar(scalars + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int d = digit_at<CB>(s, w, carry);
+      if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1) >> FB], 1u);
+    }
+  }
+  __syncthreads();
+  counts_t[(size_t)threadIdx.x * nblk + blockIdx.x] = hist[threadIdx.x];  // bin-major
+}
+
+// workgroup per coarse bin: exclusive scan of its per-block counts (bases,
+// relative to the bin start) and the bin total
+__global__ __launch_bounds__(256) void k_big2_binscan(const uint32_t* __restrict__ counts_t, uint32_t nblk,
+                                                      uint32_t* __restrict__ bases_t, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t bin = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t* src = counts_t + (size_t)bin * nblk;
+  uint32_t* dst = bases_t + (size_t)bin * nblk;
+  uint32_t run = 0;
+  for (uint32_t b0 = 0; b0 < nblk; b0 += 256) {
+    const uint32_t v = b0 + t < nblk ? src[b0 + t] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t before = run;
+    for (uint32_t w = 0; w < wv; w++) before += wsum[w];
+    if (b0 + t < nblk) dst[b0 + t] = before + x - v;
+    run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (t == 0) tot[bin] = run;
+}
+
+// one workgroup: exclusive scan of 1024 values -> out[0..1024]
+__global__ __launch_bounds__(1024) void k_scan1024(const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t v = in[t];
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (uint32_t w = 0; w < 16; w++) {
+    before += w < wv ? wsum[w] : 0u;
+    all += wsum[w];
+  }
+  out[t] = before + x - v;
+  if (t == 1023) out[1024] = all;
+}
+
+// scalars per pass-1 block: the block's W per entries are staged in LDS
+// (<= 37888 words with the 3 x 1024-word cursor arrays, gfx950's 160 KB)
+template <int CB>
+constexpr uint32_t big2_per() {
+  return Win<CB>::W <= 18 ? 2048u : 1536u;
+}
+
+// pass-1 scatter: the block's entries are ranked into LDS by coarse bin
+// (LDS atomics on local cursors), then written out in bin order -- runs of
+// consecutive positions per bin, so a wave's stores cover a few lines
+// instead of 64 scattered words (the direct scatter was write-request bound:
+// 136 us for the 2^20 + 1 MSM)
+template <int CB>
+__global__ __launch_bounds__(BIG_TPB) void k_big2_scatter(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                          const uint8_t* __restrict__ inf, uint32_t nblk,
+                                                          const uint32_t* __restrict__ counts_t,
+                                                          const uint32_t* __restrict__ coff,
+                                                          const uint32_t* __restrict__ bases_t,
+                                                          uint32_t* __restrict__ tmp, uint32_t n_rows) {
+  constexpr int W = Win<CB>::W;
+  constexpr int FB = BigFine<CB>::FB;
+  constexpr uint32_t FM = (1u << FB) - 1;
+  constexpr uint32_t PER = big2_per<CB>();
+  static_assert(BIG_TPB == BIG_NC, "thread per coarse bin");
+  __shared__ uint32_t stage[PER * W];
+  __shared__ uint32_t lstart[BIG_NC + 1], lcur[BIG_NC], gbase[BIG_NC];
+  __shared__ uint32_t wsum[BIG_TPB / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // local bin starts: exclusive scan of this block's counts (pass-1 count)
+  const uint32_t h = counts_t[(size_t)t * nblk + blockIdx.x];
+  uint32_t x = h;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  gbase[t] = coff[t] + bases_t[(size_t)t * nblk + blockIdx.x];
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (uint32_t w = 0; w < BIG_TPB / 64; w++) {
+    before += w < wv ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  lstart[t] = before + x - h;
+  lcur[t] = before + x - h;
+  if (t == 0) lstart[BIG_NC] = total;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * PER, i1 = min(n, i0 + PER);
+#pragma unroll 1
+  for (uint32_t i = i0 + t; i < i1; i += BIG_TPB) {
+    if (inf[i]) continue;
+    uint32_t s[8];
+    load_scalar(scalars + (size_t)i * 8, s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int d = digit_at<CB>(s, w, carry);
+      if (d != 0) {
+        const uint32_t bk = (uint32_t)(d < 0 ? -d : d) - 1;
+        const uint32_t pos = atomicAdd(&lcur[bk >> FB], 1u);
+        stage[pos] = ((uint32_t)w * n_rows + i) | ((bk & FM) << BIG_IDX_BITS) | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < total; j += BIG_TPB) {
+    uint32_t lo = 0, hi = BIG_NC;  // lstart[lo] <= j < lstart[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lstart[mid] <= j)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    tmp[gbase[lo] + (j - lstart[lo])] = stage[j];
+  }
+}
+
+// workgroup per coarse bin: a STABLE rank of its entries by the fine bits
+// (rounds of 256 entries in order; a wave ranks equal keys with ballots, the
+// waves in order), so every bucket keeps pass 1's block order -- ascending
+// point index -- and the threads accumulating at the same moment gather from
+// nearby table rows (an unordered rank measured the accumulation 35% slower
+// on 2^20 + 1 points: the gathers lost their L2 / MALL locality).  Also the
+// bucket offsets and each bucket's segment count ceil(len / K) (segl: the
+// bin-local exclusive prefix, segn: the bin's total).
+template <int CB>
+__global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ tmp, const uint32_t* __restrict__ coff,
+                                                   uint32_t K, uint32_t* __restrict__ entries,
+                                                   uint32_t* __restrict__ offsets, uint32_t* __restrict__ segl,
+                                                   uint32_t* __restrict__ segn) {
+  constexpr uint32_t NF = BigFine<CB>::NF;
+  constexpr int FB = BigFine<CB>::FB;
+  constexpr uint32_t NB = Win<CB>::NB;
+  constexpr uint32_t FM = NF - 1;
+  __shared__ uint32_t h[NF], cur[NF], cnt[4][NF];
+  const uint32_t bin = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t b0 = coff[bin], b1 = coff[bin + 1];
+  if (t < NF) h[t] = 0;
+  __syncthreads();
+  for (uint32_t j = b0 + t; j < b1; j += 256) atomicAdd(&h[(tmp[j] >> BIG_IDX_BITS) & FM], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = b0, sr = 0;
+    for (uint32_t f = 0; f < NF; f++) {
+      const uint32_t len = h[f];
+      offsets[bin * NF + f] = run;
+      cur[f] = run;
+      segl[bin * NF + f] = sr;
+      run += len;
+      sr += (len + K - 1) / K;
+    }
+    segn[bin] = sr;
+    if (bin == BIG_NC - 1) offsets[NB] = run;
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t r0 = b0; r0 < b1; r0 += 256) {
+    const uint32_t j = r0 + t;
+    const bool act = j < b1;
+    const uint32_t v = act ? tmp[j] : 0u;
+    const uint32_t f = (v >> BIG_IDX_BITS) & FM;
+    // lanes of this wave with the same key: AND of the per-bit ballots
+    uint64_t eq = __ballot(act);
+#pragma unroll
+    for (int b = 0; b < FB; b++) {
+      const uint64_t m = __ballot((f >> b) & 1u);
+      eq &= ((f >> b) & 1u) ? m : ~m;
+    }
+    const uint32_t rank = (uint32_t)__popcll(eq & lt);
+    if (lane < NF) cnt[wv][lane] = 0;  // this wave's counts (ordered before its own writes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (act && (eq >> lane) == 1ull) cnt[wv][f] = rank + 1;  // the last lane of its key
+    __syncthreads();  // also orders the round's reads of cur after the previous update
+    if (act) {
+      uint32_t pos = cur[f] + rank;
+      for (uint32_t w = 0; w < wv; w++) pos += cnt[w][f];
+      entries[pos] = v & (0x80000000u | ((1u << BIG_IDX_BITS) - 1u));
+    }
+    __syncthreads();
+    if (t < NF) cur[t] += cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
+    __syncthreads();
+  }
+}
+
+// segment offsets: seg_off[k] = sum over buckets j < k of ceil(len_j / K);
+// thread per coarse bin (one workgroup); *flag = some bucket has more than
+// BIG_MAXSEG segments (the reduction then pre-sums them, big_reduce_seg)
+template <int CB>
+__global__ __launch_bounds__(1024) void k_big2_segscan(const uint32_t* __restrict__ segl,
+                                                       const uint32_t* __restrict__ segn,
+                                                       uint32_t* __restrict__ seg_off, uint32_t* __restrict__ flag) {
+  constexpr uint32_t NF = BigFine<CB>::NF;
+  constexpr uint32_t NB = Win<CB>::NB;
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t any_long;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) any_long = 0;
+  const uint32_t v = segn[t];
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint32_t base = x - v;
+  for (uint32_t w = 0; w < wv; w++) base += wsum[w];
+  bool lng = false;
+  for (uint32_t f = 0; f < NF; f++) {
+    const uint32_t l = segl[t * NF + f];
+    const uint32_t nx = f + 1 < NF ? segl[t * NF + f + 1] : v;
+    lng |= nx - l > BIG_MAXSEG;
+    seg_off[t * NF + f] = base + l;
+  }
+  if (t == BIG_NC - 1) seg_off[NB] = base + v;
+  if (lng) atomicOr(&any_long, 1u);
+  __syncthreads();
+  if (t == 0) *flag = any_long;
+}
+
+// bucket k of segment j: seg_off[k] <= j < seg_off[k + 1]
+KZGX_DEV uint32_t seg_bucket(const uint32_t* __restrict__ seg_off, uint32_t nb, uint32_t j) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// thread per segment: up to K entries of one bucket, summed into part[j]
+template <class C>
+__global__ __launch_bounds__(256, pip_accum_waves<C>()) void k_big_accum(
+    const uint32_t* __restrict__ entries, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ seg_off,
+    uint32_t nb, const uint32_t* __restrict__ table, uint32_t K, uint32_t* __restrict__ part) {
+  constexpr int PW = affine_words<C>();
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= seg_off[nb]) return;
+  const uint32_t k = seg_bucket(seg_off, nb, j);
+  // the bucket's len entries in s = ceil(len / K) equal parts (not K, K, ...,
+  // rest: a wave waits for its longest thread, measured +35% on 2^20 points)
+  const uint32_t o0 = offsets[k], len = offsets[k + 1] - o0, s = seg_off[k + 1] - seg_off[k], i = j - seg_off[k];
+  const uint32_t start = o0 + (uint32_t)(((uint64_t)i * len) / s);
+  const uint32_t end = o0 + (uint32_t)(((uint64_t)(i + 1) * len) / s);
+  Xyzz<C> acc = xyzz_inf<C>();
+  // the entry and table point of p + 1 in flight during the addition of p
+  uint32_t e = entries[start];
+  uint32_t e2 = start + 1 < end ? entries[start + 1] : 0u;
+  Affine<C> nx = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+  for (uint32_t p = start; p < end; ++p) {
+    Affine<C> a = nx;
+    const uint32_t neg = e >> 31;
+    if (p + 1 < end) {
+      e = e2;
+      if (p + 2 < end) e2 = entries[p + 2];
+      nx = affine_load<C>(table + (size_t)(e & 0x7fffffffu) * PW);
+    }
+    if (neg) a = affine_neg<C>(a);
+    acc = xyzz_add_affine_impl<C>(acc, a);
+  }
+  xyzz_store<C>(part + (size_t)j * XW, acc);
+}
+
 // --------------------------------------------------------------------------
 // host side
 // --------------------------------------------------------------------------
@@ -1037,6 +1370,52 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
   const size_t nblk = (n + per - 1) / per;
   uint32_t K = ctx->seg_k;
   while (K > 8 && emax / K < 131072) K >>= 1;
+  static const bool one_pass = std::getenv("KZGX_BIG_ONEPASS") != nullptr;  // A/B: the one-pass sort + merge
+  if (!one_pass && (size_t)W * ctx->n_srs < ((size_t)1 << BIG_IDX_BITS) && n <= (size_t)65535 * 1536) {
+    const uint32_t per2 = big2_per<CB>();
+    const size_t nblk2 = (n + per2 - 1) / per2;
+    const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
+    const size_t s_ub = emax / K + NB;  // segments: sum ceil(len_k / K) <= emax / K + NB
+    WsLease wsp = ctx->ws_for(st);
+    if (!wsp) return KZGX_ERR_ARG;
+    MsmWs& ws = *wsp;
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, nblk2 * BIG_NC * 4, &ws.counts_b));
+    // bases | tot | coff | segn | flag
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, ((nblk2 + 3) * BIG_NC + 2) * 4, &ws.cursors_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, (NB + 1) * 4, &ws.offsets_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.parts, emax * 4, &ws.parts_b));  // pass-1 entries
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.entries, emax * 4, &ws.entries_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, (2 * NB + 1) * 4, &ws.tailk_b));  // seg_off | segl
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, s_ub * XB, &ws.heads_b));         // segment partials
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, big_reduce_rt_bytes(ctx->curve, NB), &ws.rt_b));
+    uint32_t* bases = ws.cursors;
+    uint32_t* tot = bases + nblk2 * BIG_NC;
+    uint32_t* coff = tot + BIG_NC;
+    uint32_t* segn = coff + BIG_NC + 1;
+    uint32_t* flag = segn + BIG_NC;
+    uint32_t* seg_off = ws.tailk;
+    uint32_t* segl = ws.tailk + NB + 1;
+    {
+      ProfScope p(ctx, st, "msm_sort");
+      hipLaunchKernelGGL(k_big2_count<CB>, dim3((unsigned)nblk2), dim3(BIG_TPB), 0, st, d_scalars, (uint32_t)n,
+                         ctx->d_inf, per2, (uint32_t)nblk2, ws.counts);
+      hipLaunchKernelGGL(k_big2_binscan, dim3(BIG_NC), dim3(256), 0, st, ws.counts, (uint32_t)nblk2, bases, tot);
+      hipLaunchKernelGGL(k_scan1024, dim3(1), dim3(1024), 0, st, tot, coff);
+      hipLaunchKernelGGL(k_big2_scatter<CB>, dim3((unsigned)nblk2), dim3(BIG_TPB), 0, st, d_scalars, (uint32_t)n,
+                         ctx->d_inf, (uint32_t)nblk2, ws.counts, coff, bases, ws.parts, (uint32_t)ctx->n_srs);
+      hipLaunchKernelGGL(k_big2_fine<CB>, dim3(BIG_NC), dim3(256), 0, st, ws.parts, coff, K, ws.entries, ws.offsets,
+                         segl, segn);
+      hipLaunchKernelGGL(k_big2_segscan<CB>, dim3(1), dim3(1024), 0, st, segl, segn, seg_off, flag);
+    }
+    {
+      ProfScope p(ctx, st, "msm_accum");
+      hipLaunchKernelGGL(k_big_accum<C>, dim3((unsigned)((s_ub + 255) / 256)), dim3(256), 0, st, ws.entries,
+                         ws.offsets, seg_off, NB, ctx->d_table_big, K, ws.heads);
+    }
+    KZGX_TRY_HIP(hipGetLastError());
+    ProfScope p(ctx, st, "msm_reduce");
+    return big_reduce_seg(ctx->curve, seg_off, ws.heads, NB, (uint32_t)s_ub, flag, ws.rt, d_out, d_out_inf, st);
+  }
   const size_t smax = (emax + K - 1) / K;
   const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);

@@ -8,7 +8,10 @@
 // every Fp product in this translation unit (wave ops, tower, curve) takes
 // the latency-first form (field29.hpp f29_mul_lat): these kernels run as one
 // wave per pairing, where a product's dependency chain is the cost
+// (KZGX_VW_CHAIN: the chained form, A/B)
+#ifndef KZGX_VW_CHAIN
 #define KZGX_FIELD_LATENCY
+#endif
 #include "pairing_common.hpp"
 #include "kzgx_setup.hpp"
 
@@ -509,7 +512,9 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
       for (int kk = 0; kk < 6; kk++) v = k == kk ? P::FROB[kk][(t == 1 || t == 2) ? 1 : 0][l] : v;
       g.v[l] = v;
     }
-    vw_st<C>(prod + lane * L, f29_mul<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
+    // the chained product form (f29_mul_chain): measured 2.90 vs 3.38 us per
+    // Frobenius against the latency-first form (profiles/r05_vw_ops_ab.json)
+    vw_st<C>(prod + lane * L, f29_mul_chain<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
   }
   __syncthreads();
   if (lane < 12) {
@@ -659,13 +664,22 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
 // no call (with its register save / restore through scratch) sits between
 // rounds.  Slots: 0 f, 1 g, 2 t0, 3 t1, 4 a, 5 b, 6 c, 7 t2, 8 t3.
 enum : uint8_t { VW_MUL, VW_CSQR, VW_CONJ, VW_FROB, VW_INV, VW_POWZ, VW_POWS, VW_POWK3 };
-// easy part f^(p^6 - 1)(p^2 + 1) -> g, then the BN254 hard part in u
+// easy part f^(p^6 - 1)(p^2 + 1) -> g, then the BN254 hard part in u, with
+// a = g^u, b = a^u, c = b^u:  f = conj(c^36 b^30 a^18 g^2)
+// (conj(c^36 b^18 a^12) g)^p (b^6 g)^(p^2) g^(p^3).  The small powers share
+// one chain per base (b^2, b^3, b^6, b^12, b^18 = b^12 b^6, b^30 = b^18 b^12;
+// a^3, a^6, a^12, a^18): 11 cyclotomic squarings + 6 products instead of
+// 22 + 8 as separate powers (round 4 form).
 __constant__ uint8_t vw_fe_bn[][4] = {
     {VW_INV, 2, 0, 0},   {VW_CONJ, 1, 0, 0},  {VW_MUL, 1, 1, 2},   {VW_FROB, 2, 1, 0},  {VW_FROB, 2, 2, 0},
     {VW_MUL, 1, 2, 1},   {VW_POWZ, 4, 1, 0},  {VW_POWZ, 5, 4, 0},  {VW_POWZ, 6, 5, 0},  {VW_POWS, 2, 6, 36},
-    {VW_POWS, 3, 5, 30}, {VW_MUL, 0, 2, 3},   {VW_POWS, 3, 4, 18}, {VW_MUL, 0, 0, 3},   {VW_CSQR, 3, 1, 0},
-    {VW_MUL, 0, 0, 3},   {VW_CONJ, 0, 0, 0},  {VW_POWS, 3, 5, 18}, {VW_POWS, 7, 4, 12}, {VW_MUL, 3, 3, 7},
-    {VW_MUL, 3, 2, 3},   {VW_CONJ, 3, 3, 0},  {VW_MUL, 3, 3, 1},   {VW_POWS, 7, 5, 6},  {VW_MUL, 7, 7, 1},
+    // b^6 -> 6, b^12 -> 7, b^18 -> 8, b^30 -> 3
+    {VW_CSQR, 6, 5, 0},  {VW_MUL, 6, 6, 5},   {VW_CSQR, 6, 6, 0},  {VW_CSQR, 7, 6, 0},  {VW_MUL, 8, 7, 6},
+    {VW_MUL, 3, 8, 7},   {VW_MUL, 0, 2, 3},
+    // a^6 -> 5, a^12 -> 7, a^18 -> 3
+    {VW_CSQR, 5, 4, 0},  {VW_MUL, 5, 5, 4},   {VW_CSQR, 5, 5, 0},  {VW_CSQR, 7, 5, 0},  {VW_MUL, 3, 7, 5},
+    {VW_MUL, 0, 0, 3},   {VW_CSQR, 3, 1, 0},  {VW_MUL, 0, 0, 3},   {VW_CONJ, 0, 0, 0},
+    {VW_MUL, 3, 8, 7},   {VW_MUL, 3, 2, 3},   {VW_CONJ, 3, 3, 0},  {VW_MUL, 3, 3, 1},   {VW_MUL, 7, 6, 1},
     {VW_FROB, 3, 3, 0},  {VW_MUL, 0, 0, 3},   {VW_FROB, 7, 7, 0},  {VW_FROB, 7, 7, 0},  {VW_MUL, 0, 0, 7},
     {VW_FROB, 8, 1, 0},  {VW_FROB, 8, 8, 0},  {VW_FROB, 8, 8, 0},  {VW_MUL, 0, 0, 8}};
 // easy part, then BLS12: t = g^K3, t2 = t^(x + p), t3 = t2^(x^2 + p^2 - 1), f = t3 g

@@ -62,5 +62,9 @@ def run(srs_n, n):
         ctx.close()
 
 
-for srs_n, n in ((131073, 131073), ((1 << 17), (1 << 17)), ((1 << 19) + 1, (1 << 19) + 1), (NMAX, NMAX)):
-    run(srs_n, n)
+SIZES = ((131073, 131073), ((1 << 17), (1 << 17)), ((1 << 19) + 1, (1 << 19) + 1), (NMAX, NMAX))
+# optional argv: the sizes to run (e.g. "1048577")
+pick = [int(a) for a in sys.argv[1:]]
+for srs_n, n in SIZES:
+    if not pick or n in pick:
+        run(srs_n, n)

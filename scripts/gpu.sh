@@ -16,6 +16,8 @@
 #   profpy:SCRIPT[,ARGS] rocprofv3 --kernel-trace --stats around python3 scripts/SCRIPT ARGS
 #   bin:PATH[,ARGS]   a built binary (e.g. kzg-commitments_amd/tools/kzg_bench)
 #   profbin:PATH[,ARGS] rocprofv3 --kernel-trace --stats around a built binary
+#   env:VAR=VALUE     export VAR for the steps that follow (A/B switches)
+#   pmcpy:CTRS:SCRIPT[,ARGS] one rocprofv3 --pmc pass around python3 scripts/SCRIPT ARGS
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 TAG=$1
@@ -92,6 +94,18 @@ for st in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/profbin_$n" -o prof --output-format csv \
         -- "./$1" "${@:2}" > "$OUT/profbin_$n.txt" 2>&1 || { tail -20 "$OUT/profbin_$n.txt"; exit 1; }
       tail -12 "$OUT/profbin_$n.txt"
+      ;;
+    pmcpy)
+      ctrs=${arg%%:*}
+      sargs=${arg#*:}
+      set -- ${sargs//,/ }
+      timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } -d "$OUT/pmcpy_$n" -o pmc --output-format csv \
+        -- python3 -u "scripts/$1" "${@:2}" > "$OUT/pmcpy_$n.txt" 2>&1 \
+        || { tail -20 "$OUT/pmcpy_$n.txt"; exit 1; }
+      ;;
+    env)
+      export "${arg?}"
+      echo "env $arg"
       ;;
     *)
       echo "unknown step $st"
