@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--fixed-bits", type=int, default=-1,
                     help="fixed-base table window (0 = Pippenger only; default BN254 17: 15 windows, "
                          "257.8 GB of 64-B entries; BLS12-381 16: 240.6 GB of 112-B entries, of the 288 GiB HBM; "
-                         "a window that does not fit steps down)")
+                         "a window that does not fit steps down; cfg5 default 0: the wide-window Pippenger)")
     ap.add_argument("--fixed-ppt", type=int, default=-1,
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic; default cfg2 22: "
                          "2048 MSMs x 3 wavefronts = two full residencies per launch; cfg4 65: 2048 x 1 wavefront; "
@@ -943,13 +943,16 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx.set_segment(args.segment)
     ctx.set_default_table(0)  # one 2^20-point MSM: its HBM goes to the shard's table
     ctx.gen_srs(tau, max(count, 1), start)
-    # fixed-base table over this rank's shard: the widest window whose table
-    # fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB; 2^19 on 2:
-    # c = 9, 249.1 GB; 2^18 on 4: c = 10, 223.3 GB; 2^17 on 8: c = 11,
-    # 206.2 GB), stored point-major (msm_fixed.hip).  Setup work, outside the
-    # timed region.
+    # Default (round 5): no fixed-base table -- the shard's MSM runs on the
+    # wide-window Pippenger path (msm.hip msm_big: c = 16 from 2^18 SRS
+    # points, 14 below; the window table is built with the SRS), which beats
+    # the c = 8 table over the whole SRS (2.2 vs 3.05 ms per 2^20 + 1 commit).
+    # --fixed-bits N: a fixed-base table over the shard, the widest window
+    # whose table fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB;
+    # 2^19 on 2: c = 9; 2^18 on 4: c = 10; 2^17 on 8: c = 11), point-major
+    # (msm_fixed.hip).  Setup work, outside the timed region.
     t_setup = time.perf_counter()
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 16
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 0
     if fixed_bits:
         fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1),
                                              budget=args.table_gb * 1e9 if args.table_gb > 0 else None)
@@ -1057,8 +1060,10 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         P_b = 2 * w64 * 8
         unit_bytes = n * (P_b + 32) + P_b
         achieved = unit_bytes / (ms_per_step * 1e-3) / 1e9
+        # the table-less window (msm.hip big_window_bits / big_min_points)
+        cbig = (16 if count >= (1 << 18) else 14) if count >= (1 << 16) else 0
         wins = ((C.r.bit_length() + fixed_bits - 1) // fixed_bits) if fixed_bits else \
-            (257 + args.window_bits - 1) // args.window_bits
+            (257 + (cbig or args.window_bits) - 1) // (cbig or args.window_bits)
         madd_rate = n * wins / (ms_per_step * 1e-3)  # all ranks' mixed additions per second
         peak = None
         try:
@@ -1105,7 +1110,8 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
                        "n_coeffs": n, "shard_points": count,
                        "msm": ("fixed-base table over the shard, c=%d, %.1f GB" % (
                            fixed_bits, ctx.fixed_base_info()[2] / 1e9)) if fixed_bits else
-                              ("pippenger, c=%d, segment %d" % (args.window_bits, args.segment)),
+                              ("wide-window pippenger, c=%d, one MSM (msm.hip msm_big)" % cbig if cbig else
+                               "pippenger, c=%d, segment %d, 4096-point chunks" % (args.window_bits, args.segment)),
                        "parallelism": "msm-shard%d" % world},
             "roofline": {
                 "kernel": "msm_accum (one MSM per rank) + all-gather + fold",

@@ -15,7 +15,7 @@
 // value bounds), the products spread over the lanes; results are the same
 // group elements (representatives may differ).  Exchange between rounds goes
 // through LDS within the wave: a wave's LDS accesses complete in program
-// order, and the wave-scope fences keep the compiler from reordering them.
+// order, and the fences (coop_fence) keep the compiler from reordering them.
 #pragma once
 #include "curve.hpp"
 
@@ -36,7 +36,10 @@ KZGX_DEV F29<F> f29_lds_ld(const uint32_t* p) {
   for (int i = 0; i < F::L; i++) a.v[i] = p[i];
   return a;
 }
-KZGX_DEV void coop_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// workgroup scope: an s_waitcnt on the LDS counter and a compiler barrier
+// (a wavefront-scope fence lowers to nothing, and nothing then stops the
+// scheduler from lifting the next round's LDS reads above this round's writes)
+KZGX_DEV void coop_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 template <class F>
 KZGX_DEV F29<F> f29_sel(bool c, const F29<F>& a, const F29<F>& b) {

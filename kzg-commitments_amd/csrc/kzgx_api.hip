@@ -1206,6 +1206,26 @@ extern "C" int kzgx_debug_latency(kzgx_ctx* ctx, int op, unsigned iters, double*
 
 // debug: latency of one wave-wide Fp12 op of the verify path
 // (verify_wave.hip k_vw_bench): res[0] = ns per op, res[1] = core clocks
+namespace kzgx {
+int coop_selftest(int curve, const uint32_t* d_tab, uint32_t n_pts, uint32_t* d_bad, hipStream_t st);  // latency.hip
+}
+// coop.hpp's cooperative point operations against the lone-lane forms on the
+// loaded SRS (window 0 of the Pippenger table); *bad = bit mask of failing cases
+extern "C" int kzgx_debug_coop_test(kzgx_ctx* ctx, unsigned* bad) {
+  KZGX_TRY(activate(ctx));
+  if (!bad || ctx->c.n_srs < 3) return KZGX_ERR_ARG;
+  uint32_t* d_bad = nullptr;
+  KZGX_TRY_HIP(hipMalloc((void**)&d_bad, 4));
+  int rc = hipMemsetAsync(d_bad, 0, 4, ctx->c.stream) == hipSuccess ? KZGX_OK : KZGX_ERR_HIP;
+  if (rc == KZGX_OK)
+    rc = kzgx::coop_selftest(ctx->c.curve, ctx->c.d_table, (uint32_t)(ctx->c.n_srs < 3 * 4096 ? ctx->c.n_srs : 3 * 4096),
+                             d_bad, ctx->c.stream);
+  if (rc == KZGX_OK && hipMemcpyAsync(bad, d_bad, 4, hipMemcpyDeviceToHost, ctx->c.stream) != hipSuccess) rc = KZGX_ERR_HIP;
+  if (rc == KZGX_OK && hipStreamSynchronize(ctx->c.stream) != hipSuccess) rc = KZGX_ERR_HIP;
+  hipFree(d_bad);
+  return rc;
+}
+
 extern "C" int kzgx_debug_vw_bench(kzgx_ctx* ctx, int op, unsigned iters, double* res) {
   KZGX_TRY(activate(ctx));
   if (!res || iters == 0) return KZGX_ERR_ARG;

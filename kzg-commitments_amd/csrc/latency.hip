@@ -93,11 +93,10 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
 constexpr uint32_t BIG_RED_J = 2;
 constexpr uint32_t BIG_F1 = 256;  // pairs per fold-1 workgroup
 
-template <class C>
+template <class C, uint32_t J>
 __global__ __launch_bounds__(256) void k_lat_bucket_sums(const uint32_t* __restrict__ offsets, uint32_t nb,
                                                          const uint32_t* __restrict__ bsum, uint32_t* __restrict__ rt) {
   constexpr int XW = xyzz_words<C>();
-  constexpr uint32_t J = BIG_RED_J;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nb / J) return;
   const uint32_t* off = offsets + (size_t)t * J;
@@ -237,7 +236,20 @@ size_t big_reduce_rt_bytes(int curve, uint32_t nb) {
 //   workgroups NGo + b:  T'_b = 2^(5 + JLOG) sum_l T_l, beside V_b's chain,
 // so the next level sees pairs (V_b, T'_b) with JLOG = 0.  Every point op is
 // one cooperative addition / doubling (~1/3 of a lone lane's latency).
-template <class C, int JLOG>
+// the fold's point ops: cooperative, or (LONE, A/B and debugging) every
+// lane of the group running the lone-lane form
+template <class C, bool LONE>
+KZGX_DEV Xyzz<C> cadd(const Xyzz<C>& a, const Xyzz<C>& b, uint32_t* sc, int j) {
+  if constexpr (LONE) return xyzz_add_impl<C>(a, b);
+  else return coop_add<C>(a, b, sc, j);
+}
+template <class C, bool LONE>
+KZGX_DEV Xyzz<C> cdbl(const Xyzz<C>& a, uint32_t* sc, int j) {
+  if constexpr (LONE) return xyzz_dbl_impl<C>(a);
+  else return coop_dbl<C>(a, sc, j);
+}
+
+template <class C, int JLOG, bool LONE>
 __global__ __launch_bounds__(256) void k_coop_fold(const uint32_t* __restrict__ in, uint32_t N, uint32_t NGo,
                                                    uint32_t* __restrict__ out) {
   using F = typename C::Fp29;
@@ -254,15 +266,15 @@ __global__ __launch_bounds__(256) void k_coop_fold(const uint32_t* __restrict__ 
   if (tpath) {
     Xyzz<C> T = idx < N ? xyzz_load<C>(src + XW) : xyzz_inf<C>();
 #pragma unroll 1
-    for (int o = 4; o >= 1; o >>= 1) T = coop_add<C>(T, xyzz_shfl_down_w<C>(T, 8 * o), my, j);
+    for (int o = 4; o >= 1; o >>= 1) T = cadd<C, LONE>(T, xyzz_shfl_down_w<C>(T, 8 * o), my, j);
     if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, T);
     __syncthreads();
     if (t >= 16) return;
     // groups 0 and 1 of wave 0: (wt0 + wt1), (wt2 + wt3); then group 0 adds
-    T = coop_add<C>(xyzz_load<C>(wt + (2 * g) * XW), xyzz_load<C>(wt + (2 * g + 1) * XW), my, j);
-    T = coop_add<C>(T, xyzz_shfl_down_w<C>(T, 8), my, j);
+    T = cadd<C, LONE>(xyzz_load<C>(wt + (2 * g) * XW), xyzz_load<C>(wt + (2 * g + 1) * XW), my, j);
+    T = cadd<C, LONE>(T, xyzz_shfl_down_w<C>(T, 8), my, j);
 #pragma unroll 1
-    for (int d = 0; d < 5 + JLOG; d++) T = coop_dbl<C>(T, my, j);
+    for (int d = 0; d < 5 + JLOG; d++) T = cdbl<C, LONE>(T, my, j);
     if (t == 0) xyzz_store<C>(out + (size_t)b * 2 * XW + XW, T);
     return;
   }
@@ -271,31 +283,31 @@ __global__ __launch_bounds__(256) void k_coop_fold(const uint32_t* __restrict__ 
 #pragma unroll 1
   for (uint32_t o = 1; o < 8; o <<= 1) {
     const Xyzz<C> x = xyzz_shfl_down_w<C>(S, (int)(8 * o));
-    if (gw + o < 8) S = coop_add<C>(S, x, my, j);
+    if (gw + o < 8) S = cadd<C, LONE>(S, x, my, j);
   }
   if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, S);
   __syncthreads();
 #pragma unroll 1
-  for (uint32_t w = wv + 1; w < 4; w++) S = coop_add<C>(S, xyzz_load<C>(wt + w * XW), my, j);
+  for (uint32_t w = wv + 1; w < 4; w++) S = cadd<C, LONE>(S, xyzz_load<C>(wt + w * XW), my, j);
   __syncthreads();  // wt is reused below
   Xyzz<C> U = R;
   if (g > 0) {
 #pragma unroll 1
-    for (int d = 0; d < JLOG; d++) S = coop_dbl<C>(S, my, j);
-    U = coop_add<C>(U, S, my, j);
+    for (int d = 0; d < JLOG; d++) S = cdbl<C, LONE>(S, my, j);
+    U = cadd<C, LONE>(U, S, my, j);
   }
 #pragma unroll 1
-  for (int o = 4; o >= 1; o >>= 1) U = coop_add<C>(U, xyzz_shfl_down_w<C>(U, 8 * o), my, j);
+  for (int o = 4; o >= 1; o >>= 1) U = cadd<C, LONE>(U, xyzz_shfl_down_w<C>(U, 8 * o), my, j);
   if ((t & 63) == 0) xyzz_store<C>(wt + wv * XW, U);
   __syncthreads();
   if (t < 8 || (t >= 128 && t < 136)) {  // group 0 of waves 0 and 2
     const Xyzz<C> o = xyzz_load<C>(wt + (wv + 1) * XW);
-    U = coop_add<C>(U, o, my, j);
+    U = cadd<C, LONE>(U, o, my, j);
     if (t == 128) xyzz_store<C>(wt + 2 * XW, U);
   }
   __syncthreads();
   if (t >= 8) return;
-  U = coop_add<C>(U, xyzz_load<C>(wt + 2 * XW), my, j);
+  U = cadd<C, LONE>(U, xyzz_load<C>(wt + 2 * XW), my, j);
   if (t == 0) xyzz_store<C>(out + (size_t)b * 2 * XW, U);
 }
 
@@ -311,9 +323,93 @@ __global__ __launch_bounds__(64) void k_coop_finish(const uint32_t* __restrict__
   *out_inf = fin ? 0u : 1u;
 }
 
-// rt holds T1 pairs (R_t, T_t) with J = 2: coop levels down to one point
+// self-test of coop.hpp against the lone-lane forms (kzgx_debug_coop_test):
+// group k takes table points a0, a1, a2 = tab[3k..3k+2] (affine Montgomery),
+// P = 2 a0 (XYZZ, ZZ != 1), Q = 2 a1 + a2, and checks coop_add(P, Q),
+// coop_add(P, P), coop_add(P, -P) and coop_dbl(Q) against xyzz_add_impl /
+// xyzz_dbl_impl in affine form; bit c of *bad set on a mismatch in case c
 template <class C>
-static int coop_levels(uint32_t* d_rt, uint32_t T1, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+__global__ __launch_bounds__(256) void k_coop_selftest(const uint32_t* __restrict__ tab, uint32_t groups,
+                                                      uint32_t* __restrict__ bad) {
+  using F = typename C::Fp29;
+  constexpr int AW = affine_words<C>();
+  __shared__ uint32_t sc[32 * COOP_SLOTS * F::L];
+  const uint32_t t = threadIdx.x, g = t >> 3;
+  const int j = (int)(t & 7);
+  const uint32_t k = blockIdx.x * 32 + g;
+  if (blockIdx.x * 32 >= groups) return;
+  const uint32_t kk = k < groups ? k : 0;
+  const Affine<C> a0 = affine_load<C>(tab + (size_t)(3 * kk) * AW);
+  const Affine<C> a1 = affine_load<C>(tab + (size_t)(3 * kk + 1) * AW);
+  const Affine<C> a2 = affine_load<C>(tab + (size_t)(3 * kk + 2) * AW);
+  const Xyzz<C> P = xyzz_dbl_impl<C>(xyzz_from_affine<C>(a0));
+  const Xyzz<C> Q = xyzz_add_affine_impl<C>(xyzz_dbl_impl<C>(xyzz_from_affine<C>(a1)), a2);
+  uint32_t* my = sc + g * COOP_SLOTS * F::L;
+  Xyzz<C> got[4], want[4];
+  got[0] = coop_add<C>(P, Q, my, j);
+  want[0] = xyzz_add_impl<C>(P, Q);
+  got[1] = coop_add<C>(P, P, my, j);
+  want[1] = xyzz_dbl_impl<C>(P);
+  got[2] = coop_add<C>(P, xyzz_neg<C>(P), my, j);
+  want[2] = xyzz_inf<C>();
+  got[3] = coop_dbl<C>(Q, my, j);
+  want[3] = xyzz_dbl_impl<C>(Q);
+  // case 4: the fold's in-wave suffix scan (shuffles between groups, groups
+  // dropping out), cooperative against every lane running the lone form
+  {
+    const uint32_t gw = (t & 63) >> 3;
+    Xyzz<C> S = Q, Sl = Q;
+#pragma unroll 1
+    for (uint32_t o = 1; o < 8; o <<= 1) {
+      const Xyzz<C> x = xyzz_shfl_down_w<C>(S, (int)(8 * o));
+      const Xyzz<C> xl = xyzz_shfl_down_w<C>(Sl, (int)(8 * o));
+      if (gw + o < 8) {
+        S = coop_add<C>(S, x, my, j);
+        Sl = xyzz_add_impl<C>(Sl, xl);
+      }
+    }
+    got[3] = coop_dbl<C>(Q, my, j);
+    want[3] = xyzz_dbl_impl<C>(Q);
+    got[2] = S;
+    want[2] = Sl;
+  }
+  if (k >= groups) return;
+  uint32_t b = 0;
+#pragma unroll 1
+  for (int c = 0; c < 4; c++) {
+    Affine<C> x, y;
+    const bool fx = xyzz_to_affine_impl<C>(got[c], x), fy = xyzz_to_affine_impl<C>(want[c], y);
+    bool same = fx == fy;
+    if (fx && fy)
+      for (int i = 0; i < F::L; i++) same = same && x.x.v[i] == y.x.v[i] && x.y.v[i] == y.y.v[i];
+    if (!same) b |= 1u << c;
+  }
+  if (b) atomicOr(bad, b);
+}
+
+int coop_selftest(int curve, const uint32_t* d_tab, uint32_t n_pts, uint32_t* d_bad, hipStream_t st) {
+  const uint32_t groups = n_pts / 3;
+  if (groups == 0) return KZGX_ERR_ARG;
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_coop_selftest<BN254G1>, dim3((groups + 31) / 32), dim3(256), 0, st, d_tab, groups, d_bad);
+  else
+    hipLaunchKernelGGL(k_coop_selftest<BLS12381G1>, dim3((groups + 31) / 32), dim3(256), 0, st, d_tab, groups, d_bad);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+template <class C, int JLOG>
+static void coop_level(const uint32_t* in, uint32_t N, uint32_t NG, uint32_t* out, hipStream_t st) {
+  static const bool lone = std::getenv("KZGX_COOP_LONE") != nullptr;
+  if (lone)
+    hipLaunchKernelGGL((k_coop_fold<C, JLOG, true>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, out);
+  else
+    hipLaunchKernelGGL((k_coop_fold<C, JLOG, false>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, out);
+}
+
+// rt holds T1 pairs (R_t, T_t) weighted V = sum_t R_t + 2^jlog t T_t
+template <class C>
+static int coop_levels(uint32_t* d_rt, uint32_t T1, int jlog, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
   constexpr int XW = xyzz_words<C>();
   uint32_t* in = d_rt;
   uint32_t* nxt = d_rt + (size_t)T1 * 2 * XW;
@@ -321,10 +417,13 @@ static int coop_levels(uint32_t* d_rt, uint32_t T1, uint32_t* d_out, uint32_t* d
   bool first = true;
   for (;;) {
     const uint32_t NG = (N + 31) / 32;
-    if (first)
-      hipLaunchKernelGGL((k_coop_fold<C, 1>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, nxt);
+    const int jl = first ? jlog : 0;
+    if (jl == 2)
+      coop_level<C, 2>(in, N, NG, nxt, st);
+    else if (jl == 1)
+      coop_level<C, 1>(in, N, NG, nxt, st);
     else
-      hipLaunchKernelGGL((k_coop_fold<C, 0>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, nxt);
+      coop_level<C, 0>(in, N, NG, nxt, st);
     first = false;
     in = nxt;
     nxt += (size_t)NG * 2 * XW;
@@ -342,7 +441,17 @@ static int big_reduce_impl(const uint32_t* d_offsets, uint32_t nb, const uint32_
   const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
   if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb in [512, 2^15]
   uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
-  hipLaunchKernelGGL(k_lat_bucket_sums<C>, dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum, d_rt);
+  static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
+  if (!lone) {
+    // 4 buckets per bucket-sum thread: half the pairs for the cooperative
+    // levels (the first level then holds 2 waves per SIMD, not 4)
+    const uint32_t T4 = nb / 4;
+    hipLaunchKernelGGL((k_lat_bucket_sums<C, 4>), dim3((T4 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum,
+                       d_rt);
+    return coop_levels<C>(d_rt, T4, 2, d_out, d_out_inf, st);
+  }
+  hipLaunchKernelGGL((k_lat_bucket_sums<C, BIG_RED_J>), dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb,
+                     d_bsum, d_rt);
   hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
   hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
   KZGX_TRY_HIP(hipGetLastError());
@@ -448,7 +557,7 @@ static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint
   // the fold: group-cooperative levels (KZGX_BIG_LONEFOLD: the lone-lane
   // k_lat_fold1 / k_lat_fold2, A/B)
   static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
-  if (!lone) return coop_levels<C>(d_rt, T1, d_out, d_out_inf, st);
+  if (!lone) return coop_levels<C>(d_rt, T1, 1, d_out, d_out_inf, st);
   hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
   hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
   KZGX_TRY_HIP(hipGetLastError());

@@ -960,8 +960,9 @@ __global__ __launch_bounds__(BIG_TPB) void k_big2_scatter(const uint32_t* __rest
 }
 
 // workgroup per coarse bin: a STABLE rank of its entries by the fine bits
-// (rounds of 256 entries in order; a wave ranks equal keys with ballots, the
-// waves in order), so every bucket keeps pass 1's block order -- ascending
+// (rounds of 1024 entries in order, 4 per thread; a wave ranks equal keys
+// with ballots, one thread per key prefixes the 16 (sub-round, wave)
+// blocks), so every bucket keeps pass 1's block order -- ascending
 // point index -- and the threads accumulating at the same moment gather from
 // nearby table rows (an unordered rank measured the accumulation 35% slower
 // on 2^20 + 1 points: the gathers lost their L2 / MALL locality).  Also the
@@ -976,7 +977,9 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
   constexpr int FB = BigFine<CB>::FB;
   constexpr uint32_t NB = Win<CB>::NB;
   constexpr uint32_t FM = NF - 1;
-  __shared__ uint32_t h[NF], cur[NF], cnt[4][NF];
+  constexpr uint32_t E = 4;  // entries per thread per round: (e, t) order, 1024 per round
+  __shared__ uint32_t h[NF], cur[NF], pre[E * 4][NF], lbase[NF], gbase[NF], stage[256 * E];
+  __shared__ uint32_t nround;
   const uint32_t bin = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t b0 = coff[bin], b1 = coff[bin + 1];
   if (t < NF) h[t] = 0;
@@ -997,31 +1000,68 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
     if (bin == BIG_NC - 1) offsets[NB] = run;
   }
   const uint64_t lt = (1ull << lane) - 1ull;
-  for (uint32_t r0 = b0; r0 < b1; r0 += 256) {
-    const uint32_t j = r0 + t;
-    const bool act = j < b1;
-    const uint32_t v = act ? tmp[j] : 0u;
-    const uint32_t f = (v >> BIG_IDX_BITS) & FM;
-    // lanes of this wave with the same key: AND of the per-bit ballots
-    uint64_t eq = __ballot(act);
+  for (uint32_t r0 = b0; r0 < b1; r0 += 256 * E) {
+    uint32_t v[E], rank[E];
 #pragma unroll
-    for (int b = 0; b < FB; b++) {
-      const uint64_t m = __ballot((f >> b) & 1u);
-      eq &= ((f >> b) & 1u) ? m : ~m;
+    for (uint32_t e = 0; e < E; e++) {
+      const uint32_t j = r0 + e * 256 + t;
+      const bool act = j < b1;
+      v[e] = act ? tmp[j] : 0u;
+      const uint32_t f = (v[e] >> BIG_IDX_BITS) & FM;
+      // lanes of this wave with the same key: AND of the per-bit ballots
+      uint64_t eq = __ballot(act);
+#pragma unroll
+      for (int b = 0; b < FB; b++) {
+        const uint64_t m = __ballot((f >> b) & 1u);
+        eq &= ((f >> b) & 1u) ? m : ~m;
+      }
+      rank[e] = act ? (uint32_t)__popcll(eq & lt) : ~0u;
+      if (lane < NF) pre[e * 4 + wv][lane] = 0;  // this wave's counts (ordered before its own writes)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (act && (eq >> lane) == 1ull) pre[e * 4 + wv][f] = rank[e] + 1;  // the last lane of its key
     }
-    const uint32_t rank = (uint32_t)__popcll(eq & lt);
-    if (lane < NF) cnt[wv][lane] = 0;  // this wave's counts (ordered before its own writes)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (act && (eq >> lane) == 1ull) cnt[wv][f] = rank + 1;  // the last lane of its key
-    __syncthreads();  // also orders the round's reads of cur after the previous update
-    if (act) {
-      uint32_t pos = cur[f] + rank;
-      for (uint32_t w = 0; w < wv; w++) pos += cnt[w][f];
-      entries[pos] = v & (0x80000000u | ((1u << BIG_IDX_BITS) - 1u));
+    __syncthreads();  // also orders this round's reads of cur after the previous update
+    if (t < 64) {  // wave 0: per key, the 16 blocks' local prefix, the key's round total, then a
+                   // scan over the keys -> each key's start in the round (sorted by key)
+      uint32_t tot = 0;
+      if (t < NF) {
+#pragma unroll
+        for (uint32_t q = 0; q < E * 4; q++) {
+          const uint32_t c = pre[q][t];
+          pre[q][t] = tot;
+          tot += c;
+        }
+      }
+      uint32_t x = tot;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      if (t < NF) {
+        lbase[t] = x - tot;
+        gbase[t] = cur[t];
+        cur[t] += tot;
+      }
+      const uint32_t all = __shfl(x, (int)NF - 1, 64);
+      if (t == 0) nround = all;
     }
     __syncthreads();
-    if (t < NF) cur[t] += cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {
+      if (rank[e] == ~0u) continue;
+      const uint32_t f = (v[e] >> BIG_IDX_BITS) & FM;
+      stage[lbase[f] + pre[e * 4 + wv][f] + rank[e]] = v[e];
+    }
     __syncthreads();
+    // write the round sorted by key: consecutive threads, consecutive
+    // positions of each key's run (a wave's stores cover a few lines)
+    for (uint32_t q = t; q < nround; q += 256) {
+      const uint32_t w = stage[q];
+      const uint32_t f = (w >> BIG_IDX_BITS) & FM;
+      entries[gbase[f] + (q - lbase[f])] = w & (0x80000000u | ((1u << BIG_IDX_BITS) - 1u));
+    }
+    __syncthreads();  // pre, stage and the bases are rewritten by the next round
   }
 }
 
@@ -1380,21 +1420,18 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     if (!wsp) return KZGX_ERR_ARG;
     MsmWs& ws = *wsp;
     KZGX_TRY(dev_alloc(ctx, (void**)&ws.counts, nblk2 * BIG_NC * 4, &ws.counts_b));
-    // bases | tot | coff | segn | flag
-    KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, ((nblk2 + 3) * BIG_NC + 2) * 4, &ws.cursors_b));
+    // bases | tot | coff | segn | flag | segl
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.cursors, ((nblk2 + 3) * BIG_NC + 2 + NB) * 4, &ws.cursors_b));
     KZGX_TRY(dev_alloc(ctx, (void**)&ws.offsets, (NB + 1) * 4, &ws.offsets_b));
     KZGX_TRY(dev_alloc(ctx, (void**)&ws.parts, emax * 4, &ws.parts_b));  // pass-1 entries
     KZGX_TRY(dev_alloc(ctx, (void**)&ws.entries, emax * 4, &ws.entries_b));
-    KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, (2 * NB + 1) * 4, &ws.tailk_b));  // seg_off | segl
-    KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, s_ub * XB, &ws.heads_b));         // segment partials
     KZGX_TRY(dev_alloc(ctx, (void**)&ws.rt, big_reduce_rt_bytes(ctx->curve, NB), &ws.rt_b));
     uint32_t* bases = ws.cursors;
     uint32_t* tot = bases + nblk2 * BIG_NC;
     uint32_t* coff = tot + BIG_NC;
     uint32_t* segn = coff + BIG_NC + 1;
     uint32_t* flag = segn + BIG_NC;
-    uint32_t* seg_off = ws.tailk;
-    uint32_t* segl = ws.tailk + NB + 1;
+    uint32_t* segl = flag + 2;
     {
       ProfScope p(ctx, st, "msm_sort");
       hipLaunchKernelGGL(k_big2_count<CB>, dim3((unsigned)nblk2), dim3(BIG_TPB), 0, st, d_scalars, (uint32_t)n,
@@ -1405,16 +1442,57 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
                          ctx->d_inf, (uint32_t)nblk2, ws.counts, coff, bases, ws.parts, (uint32_t)ctx->n_srs);
       hipLaunchKernelGGL(k_big2_fine<CB>, dim3(BIG_NC), dim3(256), 0, st, ws.parts, coff, K, ws.entries, ws.offsets,
                          segl, segn);
-      hipLaunchKernelGGL(k_big2_segscan<CB>, dim3(1), dim3(1024), 0, st, segl, segn, seg_off, flag);
     }
+    // accumulation: K-entry segments across bucket boundaries with the
+    // merge of crossing partials, or bucket-aligned segments summed by the
+    // reduction (no merge, but measured 1.83 vs 1.31 ms of accumulation on
+    // 2^20 + 1 points at the same VALU count and cache hit rate,
+    // profiles/r05_big_msm_pmc.json -- an unexplained gap, left measured)
+    // (KZGX_BIG_SEGACC=0/1 pins it; by default bucket-aligned segments when K
+    // was cut to <= 32 to spread a smaller MSM: buckets then span ~20
+    // segments and the merge's chains dominate -- 131 073 points 0.64 vs
+    // 0.84 ms, while 2^20 + 1 points take 2.20 vs 2.62 ms with the merge)
+    static const char* seg_env = std::getenv("KZGX_BIG_SEGACC");
+    const bool seg_acc = seg_env ? seg_env[0] == '1' : K <= 32;
+    if (seg_acc) {
+      KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, (NB + 1) * 4, &ws.tailk_b));  // seg_off
+      KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, s_ub * XB, &ws.heads_b));     // segment partials
+      uint32_t* seg_off = ws.tailk;
+      hipLaunchKernelGGL(k_big2_segscan<CB>, dim3(1), dim3(1024), 0, st, segl, segn, seg_off, flag);
+      {
+        ProfScope p(ctx, st, "msm_accum");
+        hipLaunchKernelGGL(k_big_accum<C>, dim3((unsigned)((s_ub + 255) / 256)), dim3(256), 0, st, ws.entries,
+                           ws.offsets, seg_off, NB, ctx->d_table_big, K, ws.heads);
+      }
+      KZGX_TRY_HIP(hipGetLastError());
+      ProfScope p(ctx, st, "msm_reduce");
+      return big_reduce_seg(ctx->curve, seg_off, ws.heads, NB, (uint32_t)s_ub, flag, ws.rt, d_out, d_out_inf, st);
+    }
+    const size_t smax2 = (emax + K - 1) / K;
+    const size_t nwg2 = (smax2 + ACC_WG - 1) / ACC_WG;
+    if (nwg2 > 65535) return KZGX_ERR_ARG;
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.bsum, NB * XB, &ws.bsum_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.heads, smax2 * XB, &ws.heads_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.tails, smax2 * XB, &ws.tails_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.tailk, smax2 * 4, &ws.tailk_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.sstate, smax2, &ws.sstate_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.gpart, nwg2 * 2 * XB, &ws.gpart_b));
+    KZGX_TRY(dev_alloc(ctx, (void**)&ws.gmeta, nwg2 * 2 * 4, &ws.gmeta_b));
     {
       ProfScope p(ctx, st, "msm_accum");
-      hipLaunchKernelGGL(k_big_accum<C>, dim3((unsigned)((s_ub + 255) / 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, seg_off, NB, ctx->d_table_big, K, ws.heads);
+      hipLaunchKernelGGL(k_msm_accum<C>, dim3((unsigned)((smax2 + 255) / 256), 1), dim3(256), 0, st, ws.entries, emax,
+                         ws.offsets, NB, ctx->d_table_big, K, (uint32_t)smax2, ws.bsum, ws.heads, ws.tails, ws.tailk,
+                         ws.sstate);
     }
-    KZGX_TRY_HIP(hipGetLastError());
     ProfScope p(ctx, st, "msm_reduce");
-    return big_reduce_seg(ctx->curve, seg_off, ws.heads, NB, (uint32_t)s_ub, flag, ws.rt, d_out, d_out_inf, st);
+    uint32_t* gh = ws.gpart;
+    uint32_t* gt = ws.gpart + nwg2 * xyzz_words<C>();
+    hipLaunchKernelGGL(k_msm_merge<C>, dim3((unsigned)nwg2, 1), dim3(ACC_WG), 0, st, ws.heads, ws.tails, ws.tailk,
+                       ws.sstate, (uint32_t)smax2, NB, (uint32_t)nwg2, ws.bsum, gh, gt, ws.gmeta, ws.gmeta + nwg2);
+    hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg2 + 63) / 64), 1), dim3(64), 0, st, NB, (uint32_t)nwg2,
+                       gh, gt, ws.gmeta, ws.gmeta + nwg2, ws.bsum);
+    KZGX_TRY_HIP(hipGetLastError());
+    return big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st);
   }
   const size_t smax = (emax + K - 1) / K;
   const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
