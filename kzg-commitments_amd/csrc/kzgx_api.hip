@@ -5,6 +5,8 @@
 // kzgx_create fails with KZGX_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <array>
 
 #include <algorithm>
@@ -49,6 +51,66 @@ namespace kzgx {
 
 int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? KZGX_ERR_OOM : KZGX_ERR_HIP; }
 
+// One cached table block per device: the last large fixed-base / default
+// table freed (a context destroyed) is kept for the next context's table of
+// (about) the same size.  A trusted_setup per degree (the reference
+// benchmark, benchmark/benchmark.cpp:19-38) otherwise frees and re-allocates
+// an 11.8 GB default table each time, and one such hipMalloc in a few took
+// 5.3-5.8 s (profiles/r05_kzg_bench_cpp.txt: the 512-term setup; the bench's
+// setup leg).  The block is released before any allocation it cannot serve
+// and on any allocation failure; KZGX_NO_TABLE_CACHE=1 turns the cache off.
+namespace {
+struct TableBlock {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_table_mu;
+TableBlock g_table_cache[64];
+bool table_cache_off() {
+  static const bool off = std::getenv("KZGX_NO_TABLE_CACHE") && std::getenv("KZGX_NO_TABLE_CACHE")[0] == '1';
+  return off;
+}
+}  // namespace
+
+void table_cache_release() {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  TableBlock& b = g_table_cache[dev];
+  if (b.p) (void)hipFree(b.p);
+  b = TableBlock{};
+}
+
+hipError_t table_malloc(void** p, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    TableBlock& b = g_table_cache[dev];
+    if (b.p && b.bytes >= bytes && b.bytes - bytes <= bytes / 4) {
+      *p = b.p;
+      b = TableBlock{};
+      return hipSuccess;
+    }
+    if (b.p) (void)hipFree(b.p);  // never hold a block beside a new allocation
+    b = TableBlock{};
+  }
+  return hipMalloc(p, bytes);
+}
+
+void table_free(void* p, size_t bytes) {
+  if (!p) return;
+  int dev = 0;
+  if (table_cache_off() || bytes < ((size_t)1 << 30) || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipFree(p);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  TableBlock& b = g_table_cache[dev];
+  if (b.p) (void)hipFree(b.p);
+  b.p = p;
+  b.bytes = bytes;
+}
+
 int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap) {
   (void)ctx;
   if (bytes == 0) bytes = 16;
@@ -64,6 +126,7 @@ int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap) {
   hipError_t e = hipMalloc(p, want);
   if (e != hipSuccess) {
     *p = nullptr;
+    table_cache_release();  // a cached table block may be what is missing
     e = hipMalloc(p, bytes);
     if (e != hipSuccess) {
       *p = nullptr;
@@ -1222,7 +1285,7 @@ extern "C" int kzgx_debug_coop_test(kzgx_ctx* ctx, unsigned* bad) {
                              d_bad, ctx->c.stream);
   if (rc == KZGX_OK && hipMemcpyAsync(bad, d_bad, 4, hipMemcpyDeviceToHost, ctx->c.stream) != hipSuccess) rc = KZGX_ERR_HIP;
   if (rc == KZGX_OK && hipStreamSynchronize(ctx->c.stream) != hipSuccess) rc = KZGX_ERR_HIP;
-  hipFree(d_bad);
+  (void)hipFree(d_bad);
   return rc;
 }
 

@@ -1195,20 +1195,11 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   hipLaunchKernelGGL(k_srs_to_mont<C>, grd, blk, 0, ctx->stream, d_canon, ctx->d_table, ctx->d_inf, (uint32_t)n);
   hipLaunchKernelGGL(k_table_build<C>, grd, blk, 0, ctx->stream, ctx->d_table, ctx->d_inf, (uint32_t)n, W, ctx->c);
   KZGX_TRY_HIP(hipGetLastError());
+  // the small-batch window table is built on first use (small_table_ready):
+  // only table-off single calls and small batches read it, and a setup whose
+  // calls all take the default table never pays its ~2.6 ms latency-bound
+  // build (the reference benchmark's 128-term setup)
   ctx->n_small = 0;
-  if (ctx->c != KZGX_SMALL_WINDOW_BITS) {
-    // window 0 of the small table is the Montgomery SRS prefix (window 0 of
-    // the main table); k_table_build derives the others
-    const size_t ns = n < SMALL_MAX_POINTS ? n : SMALL_MAX_POINTS;
-    constexpr int WS = Win<KZGX_SMALL_WINDOW_BITS>::W;
-    KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_small, (size_t)WS * ns * pw, &ctx->table_small_bytes));
-    KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_small, ctx->d_table, ns * pw, hipMemcpyDeviceToDevice, ctx->stream));
-    dim3 grs((unsigned)((ns + 255) / 256));
-    hipLaunchKernelGGL(k_table_build<C>, grs, blk, 0, ctx->stream, ctx->d_table_small, ctx->d_inf, (uint32_t)ns, WS,
-                       KZGX_SMALL_WINDOW_BITS);
-    KZGX_TRY_HIP(hipGetLastError());
-    ctx->n_small = ns;
-  }
   // the wide-window table of the large single MSMs (window 0 = the
   // Montgomery SRS, window 0 of the main table)
   ctx->c_big = 0;
@@ -1341,12 +1332,33 @@ int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
                                         : srs_upload_impl<BLS12381G1>(ctx, d_canon, n);
 }
 
+// window 0 of the small table is the Montgomery SRS prefix (window 0 of the
+// main table); k_table_build derives the others.  Built on the calling
+// stream and waited for once, so calls on other streams never see it half
+// built.
+template <class C>
+static int small_table_ready(Ctx* ctx, hipStream_t st) {
+  if (ctx->n_small || ctx->c == KZGX_SMALL_WINDOW_BITS || !ctx->n_srs || !ctx->d_table) return KZGX_OK;
+  const size_t pw = affine_words<C>() * sizeof(uint32_t);
+  const size_t ns = ctx->n_srs < SMALL_MAX_POINTS ? ctx->n_srs : SMALL_MAX_POINTS;
+  constexpr int WS = Win<KZGX_SMALL_WINDOW_BITS>::W;
+  KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_small, (size_t)WS * ns * pw, &ctx->table_small_bytes));
+  KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_small, ctx->d_table, ns * pw, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(k_table_build<C>, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, ctx->d_table_small,
+                     ctx->d_inf, (uint32_t)ns, WS, KZGX_SMALL_WINDOW_BITS);
+  KZGX_TRY_HIP(hipGetLastError());
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  ctx->n_small = ns;
+  return KZGX_OK;
+}
+
 template <class C>
 static int msm_batch_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
                        uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t point_base,
                        uint32_t point_stride, uint32_t* xyzz_out) {
   // small batches inside the small table's prefix: the short-reduction window
   const size_t last = (size_t)point_base + (batch ? (batch - 1) * (size_t)point_stride : 0) + n;
+  if (batch <= ctx->small_batch && last <= SMALL_MAX_POINTS) KZGX_TRY(small_table_ready<C>(ctx, st));
   if (ctx->n_small && batch <= ctx->small_batch && last <= ctx->n_small)
     return msm_batch_impl<C, KZGX_SMALL_WINDOW_BITS>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st,
                                                      point_base, point_stride, xyzz_out, ctx->d_table_small,

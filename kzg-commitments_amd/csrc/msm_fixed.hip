@@ -64,6 +64,24 @@ __global__ __launch_bounds__(64) void k_fixed_bases(const uint32_t* __restrict__
   }
 }
 
+// the same bases from the Pippenger window table when it has the fixed
+// table's window (T[w][i] = 2^(c w) P_i, msm.hip k_table_build): a copy into
+// the packed layout instead of each point's chain of c (W - 1) doublings and
+// W - 1 inversions (2.4 ms for any SRS size, latency-bound)
+template <class C>
+__global__ __launch_bounds__(256) void k_fixed_bases_from_table(const uint32_t* __restrict__ table,
+                                                                const uint8_t* __restrict__ inf_src, uint32_t n,
+                                                                uint32_t n_rows, int W, uint32_t* __restrict__ bases,
+                                                                uint8_t* __restrict__ inf) {
+  constexpr int PW = packed_words<C>();
+  constexpr int AW = affine_words<C>();
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (uint64_t)W * n) return;
+  const uint32_t w = (uint32_t)(g / n), i = (uint32_t)(g % n);
+  packed_store<C>(bases + g * PW, affine_load<C>(table + ((size_t)w * n_rows + i) * AW));
+  if (w == 0) inf[i] = inf_src[i];
+}
+
 // M(w, i, j0 + j) = (2 (j0 + j) + 1) B[w][i], j < J (the odd multiples the
 // regular odd digits index, fixed_accum.hpp); thread per (w, i, block),
 // written at the table's strides (TabStrides)
@@ -561,6 +579,10 @@ static TabStrides tab_strides(const FixedTable& ft) {
 // the infinity flags the accumulation kernels read, or null when none is set
 static const uint8_t* fixed_inf(const FixedTable& ft) { return ft.any_inf ? ft.inf : nullptr; }
 
+// the per-device cached table block (kzgx_api.hip)
+hipError_t table_malloc(void** p, size_t bytes);
+void table_free(void* p, size_t bytes);
+
 template <class C>
 static int fixed_build_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, size_t n) {
   const int c = ft.c_req;
@@ -588,15 +610,19 @@ static int fixed_build_impl(Ctx* ctx, FixedTable& ft, const uint32_t* d_canon, s
       }
     }
   } g{ft};
-  KZGX_TRY_HIP(hipMalloc((void**)&ft.d, bytes));
+  KZGX_TRY_HIP(table_malloc((void**)&ft.d, bytes));
   ft.bytes = bytes;
   KZGX_TRY_HIP(hipMalloc((void**)&g.bases, (size_t)W * n * PB));
   KZGX_TRY_HIP(hipMalloc((void**)&g.inf, n));
   uint32_t* d_bases = g.bases;
   uint8_t* d_inf = g.inf;
   hipStream_t st = ctx->stream;
-  hipLaunchKernelGGL(k_fixed_bases<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_canon, (uint32_t)n, W, c,
-                     d_bases, d_inf);
+  if (ctx->d_table && ctx->c == c && W <= ctx->W && n <= ctx->n_srs)
+    hipLaunchKernelGGL(k_fixed_bases_from_table<C>, dim3((unsigned)(((uint64_t)W * n + 255) / 256)), dim3(256), 0, st,
+                       ctx->d_table, ctx->d_inf, (uint32_t)n, (uint32_t)ctx->n_srs, W, d_bases, d_inf);
+  else
+    hipLaunchKernelGGL(k_fixed_bases<C>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_canon, (uint32_t)n, W, c,
+                       d_bases, d_inf);
   ft.point_major = fixed_point_major(c, ft.layout_req);
   const TabStrides ts = fixed_strides<C>(ft.point_major, W, n, H);
   // KZGX_TABLE_BUILD_SERIAL=1: the round-4 builder (one inversion per entry),
@@ -692,7 +718,7 @@ int fixed_rebuild_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) {
 void fixed_free(Ctx* ctx) { fixed_free_table(ctx->fixed); }
 
 void fixed_free_table(FixedTable& ft) {
-  if (ft.d) (void)hipFree(ft.d);
+  if (ft.d) table_free(ft.d, ft.bytes);
   if (ft.inf) (void)hipFree(ft.inf);
   ft.d = nullptr;
   ft.inf = nullptr;

@@ -361,7 +361,12 @@ __global__ __launch_bounds__(64) void k_fixed_multiples_batch(const uint32_t* __
 
 int fixed_multiples_batch(int curve, const uint32_t* d_bases, const uint8_t* d_inf, uint32_t n, int W, uint32_t H,
                           size_t is, size_t ws, uint32_t* d_tab, hipStream_t st) {
-  const uint32_t per = H < FM_PER ? H : FM_PER;
+  // entries per thread: FM_PER, halved (down to the K chains) while the
+  // grid would hold fewer than 64k threads -- a small SRS (the 129-point
+  // setup: 5.8 M entries, 5.6 k threads of 1024) is otherwise one long
+  // latency-bound chain per thread (8.2 ms -> ~1 ms)
+  uint32_t per = H < FM_PER ? H : FM_PER;
+  while (per > (uint32_t)FM_K && (uint64_t)W * n * (H / per) < 65536) per >>= 1;
   const uint64_t tasks = (uint64_t)W * n * (H / per);
   const TabStrides ts{is, ws};
   // bounded launches, synchronised per slice so one setup never queues

@@ -17,6 +17,7 @@
 #   bin:PATH[,ARGS]   a built binary (e.g. kzg-commitments_amd/tools/kzg_bench)
 #   profbin:PATH[,ARGS] rocprofv3 --kernel-trace --stats around a built binary
 #   env:VAR=VALUE     export VAR for the steps that follow (A/B switches)
+#   tracebin:PATH[,ARGS] kernel + HIP runtime API trace around a built binary
 #   pmcpy:CTRS:SCRIPT[,ARGS] one rocprofv3 --pmc pass around python3 scripts/SCRIPT ARGS
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -102,6 +103,12 @@ for st in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } -d "$OUT/pmcpy_$n" -o pmc --output-format csv \
         -- python3 -u "scripts/$1" "${@:2}" > "$OUT/pmcpy_$n.txt" 2>&1 \
         || { tail -20 "$OUT/pmcpy_$n.txt"; exit 1; }
+      ;;
+    tracebin)
+      set -- ${arg//,/ }
+      timeout -k 10 600 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d "$OUT/tracebin_$n" -o trace \
+        --output-format csv -- "./$1" "${@:2}" > "$OUT/tracebin_$n.txt" 2>&1 || { tail -20 "$OUT/tracebin_$n.txt"; exit 1; }
+      tail -12 "$OUT/tracebin_$n.txt"
       ;;
     env)
       export "${arg?}"
