@@ -83,9 +83,10 @@ def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
     if world == 1:
         return packed
     g = torch.empty((world, packed.shape[0]), dtype=packed.dtype, device=packed.device)
-    if hasattr(dist, "all_gather_into_tensor") and packed.device.type == "cuda":
-        dist.all_gather_into_tensor(g, packed)
-    else:  # gloo has no all_gather_into_tensor
+    backend = dist.get_backend() if hasattr(dist, "get_backend") else None
+    if backend == "nccl" and hasattr(dist, "all_gather_into_tensor"):
+        dist.all_gather_into_tensor(g, packed)  # RCCL: straight into the (world, W) tensor
+    else:  # gloo (the one-box rehearsal, CPU tests): list form into the rows of g
         outs = list(g.unbind(0))
         dist.all_gather(outs, packed)
     mark("gather")
