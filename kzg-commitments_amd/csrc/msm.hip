@@ -1047,13 +1047,23 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
     if (bin == BIG_NC - 1) offsets[NB] = run;
   }
   const uint64_t lt = (1ull << lane) - 1ull;
+  // the next round's entries are loaded while this round ranks (its global
+  // loads no longer sit between rounds)
+  uint32_t vn[E];
+#pragma unroll
+  for (uint32_t e = 0; e < E; e++) vn[e] = b0 + e * 256 + t < b1 ? tmp[b0 + e * 256 + t] : 0u;
   for (uint32_t r0 = b0; r0 < b1; r0 += 256 * E) {
     uint32_t v[E], rank[E];
 #pragma unroll
     for (uint32_t e = 0; e < E; e++) {
+      v[e] = vn[e];
+      const uint32_t jn = r0 + 256 * E + e * 256 + t;
+      vn[e] = jn < b1 ? tmp[jn] : 0u;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {
       const uint32_t j = r0 + e * 256 + t;
       const bool act = j < b1;
-      v[e] = act ? tmp[j] : 0u;
       const uint32_t f = (v[e] >> BIG_IDX_BITS) & FM;
       // lanes of this wave with the same key: AND of the per-bit ballots
       uint64_t eq = __ballot(act);

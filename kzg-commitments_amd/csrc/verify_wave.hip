@@ -61,8 +61,11 @@ struct VWave {
   // LDS carve (words)
   static constexpr int O_LINES = 0;                        // [2][NL][LW] scaled lines
   static constexpr int O_SLOT = O_LINES + 2 * NL * LW;     // [NSLOT][E12]
-  static constexpr int O_PROD = O_SLOT + NSLOT * E12;      // [36][E2] products; G1 phase: [32][4L] XYZZ tree
-  static constexpr int PROD_W = (36 * E2 > 32 * 4 * L) ? 36 * E2 : 32 * 4 * L;
+  // product parts at a 16-byte stride PL >= L, so a part is written and
+  // read back with 128-bit LDS accesses (the folds read 7-18 parts per lane)
+  static constexpr int PL = (L + 3) & ~3;
+  static constexpr int O_PROD = O_SLOT + NSLOT * E12;      // [108][PL] product parts; G1 phase: [32][4L] XYZZ tree
+  static constexpr int PROD_W = (108 * PL > 32 * 4 * L) ? 108 * PL : 32 * 4 * L;
   static constexpr int O_SCALE = O_PROD + PROD_W;          // [2][3][L] scale factors
   static constexpr int O_FLAG = O_SCALE + 6 * L;           // [16]
   static constexpr int WORDS = O_FLAG + 16;
@@ -265,6 +268,44 @@ KZGX_DEV void lin_add_f2(LinAcc<F>& acc, const uint32_t* q, int im, bool xi, int
   lin_add<F>(acc, q + 2 * L, d * c2);
 }
 
+// product parts (16-byte aligned, stride VWave::PL): 128-bit LDS accesses
+template <class C>
+KZGX_DEV void vw_stp(uint32_t* p, const F29<typename C::Fp29>& a) {
+  constexpr int L = C::Fp29::L;
+#pragma unroll
+  for (int i = 0; i + 4 <= L; i += 4)
+    *reinterpret_cast<uint4*>(p + i) = make_uint4(a.v[i], a.v[i + 1], a.v[i + 2], a.v[i + 3]);
+#pragma unroll
+  for (int i = L & ~3; i < L; i++) p[i] = a.v[i];
+}
+template <class F>
+KZGX_DEV void lin_addp(LinAcc<F>& a, const uint32_t* p, int c) {
+  constexpr int L = F::L;
+  uint32_t w[L];
+#pragma unroll
+  for (int i = 0; i + 4 <= L; i += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+    w[i] = q.x;
+    w[i + 1] = q.y;
+    w[i + 2] = q.z;
+    w[i + 3] = q.w;
+  }
+#pragma unroll
+  for (int i = L & ~3; i < L; i++) w[i] = p[i];
+#pragma unroll
+  for (int l = 0; l < L; l++) a.v[l] += (int64_t)(int32_t)w[l] * (int64_t)c;
+}
+// lin_add_f2 over a part triple at stride PL
+template <class F, int PL>
+KZGX_DEV void lin_add_f2p(LinAcc<F>& acc, const uint32_t* q, int im, bool xi, int d) {
+  const int c0 = xi ? (im ? 0 : 2) : (im ? -1 : 1);
+  const int c1 = xi ? (im ? -2 : 0) : -1;
+  const int c2 = xi ? (im ? 1 : -1) : (im ? 1 : 0);
+  lin_addp<F>(acc, q, d * c0);
+  lin_addp<F>(acc, q + PL, d * c1);
+  lin_addp<F>(acc, q + 2 * PL, d * c2);
+}
+
 // ---- Fp12 (w basis) in LDS, wave-cooperative; every op ends with a barrier
 // dst = a b (dst may alias a or b): the 36 Fp2 products a_i b_j as 108 Fp
 // (Karatsuba) parts, two independent products per lane (54 lanes), then lane
@@ -275,13 +316,13 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t *a = vw_smem + a_o, *b = vw_smem + b_o;
   using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   const int lane = threadIdx.x;
   if (lane < 54) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int t = lane + 54 * h, pr = t / 3;
-      vw_st<C>(prod + t * L, vw_part<C>(vw_ld2<C>(a + (pr / 6) * E2), vw_ld2<C>(b + (pr % 6) * E2), t % 3));
+      vw_stp<C>(prod + t * PL, vw_part<C>(vw_ld2<C>(a + (pr / 6) * E2), vw_ld2<C>(b + (pr % 6) * E2), t % 3));
     }
   }
   __syncthreads();
@@ -294,7 +335,7 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
     for (int i = 0; i < 6; i++) {
       const bool wrap = i > k;
       const int j = wrap ? k + 6 - i : k - i;
-      lin_add_f2<F>(acc, prod + (i * 6 + j) * 3 * L, im, wrap, 1);
+      lin_add_f2p<F, PL>(acc, prod + (i * 6 + j) * 3 * PL, im, wrap, 1);
     }
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -309,13 +350,13 @@ template <class C>
 KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o) {
   using F = typename C::Fp29;
   using V = VWave<C>;
-  constexpr int E2 = V::E2, L = V::L;
+  constexpr int E2 = V::E2, L = V::L, PL = V::PL;
   uint32_t *f = vw_smem + f_o, *prod = vw_smem + prod_o;
   const uint32_t* line = vw_smem + line_o;
   const int lane = threadIdx.x;
   if (lane < 54) {
     const int i = lane / 9, t = (lane / 3) % 3;
-    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(f + i * E2), vw_ld2<C>(line + t * E2), lane % 3));
+    vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(f + i * E2), vw_ld2<C>(line + t * E2), lane % 3));
   }
   __syncthreads();
   if (lane < 12) {
@@ -328,7 +369,7 @@ KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o) {
       int i = k - pos;
       const bool wrap = i < 0;
       if (wrap) i += 6;
-      lin_add_f2<F>(acc, prod + (i * 9 + t * 3) * L, im, wrap, 1);
+      lin_add_f2p<F, PL>(acc, prod + (i * 9 + t * 3) * PL, im, wrap, 1);
     }
     vw_st<C>(f + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -345,7 +386,7 @@ KZGX_DEV int vw_pair_index(int i, int j) {
 template <class C>
 KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t* a = vw_smem + a_o;
   const int lane = threadIdx.x;
@@ -355,7 +396,7 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
       idx -= 6 - i;
       i++;
     }
-    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(a + (i + idx) * E2), lane % 3));
+    vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(a + (i + idx) * E2), lane % 3));
   }
   __syncthreads();
   if (lane < 12) {
@@ -371,7 +412,7 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
       const bool wrap = i > k;
       const int j = wrap ? k + 6 - i : k - i;
       const int lo = i < j ? i : j, hi = i < j ? j : i;
-      lin_add_f2<F>(acc, prod + 3 * vw_pair_index<C>(lo, hi) * L, im, wrap, 1);
+      lin_add_f2p<F, PL>(acc, prod + 3 * vw_pair_index<C>(lo, hi) * PL, im, wrap, 1);
     }
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -408,7 +449,7 @@ KZGX_DEV F29<F> vw_norm(const uint32_t (&o)[F::L]) {
 template <class C>
 KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t* a = vw_smem + a_o;
   const int lane = threadIdx.x;
@@ -428,13 +469,13 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
       const uint32_t u1 = sx + ya + (ya & y2) + ((F::P2B[l] - yb) & yn) + (yb & yp1);
       o1[l] = which ? u1 : sy;
     }
-    vw_st<C>(prod + lane * L, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
+    vw_stp<C>(prod + lane * PL, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
   }
   __syncthreads();
   if (lane < 12) {
     const int k = lane >> 1, im = lane & 1;
     const int j = (k & 1) ? (k == 3 ? 0 : k == 5 ? 1 : 2) : (k >> 1);
-    const uint32_t* q = prod + j * 6 * L;
+    const uint32_t* q = prod + j * 6 * PL;
     int cp0, cp1, cp2, cq0 = 0, cq1 = 0, cq2 = 0;
     if (!(k & 1)) {
       cp0 = im ? 1 : -3;
@@ -454,12 +495,12 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     }
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add<F>(acc, q, 3 * cp0);
-    lin_add<F>(acc, q + L, 3 * cp1);
-    lin_add<F>(acc, q + 2 * L, 3 * cp2);
-    lin_add<F>(acc, q + 3 * L, 3 * cq0);
-    lin_add<F>(acc, q + 4 * L, 3 * cq1);
-    lin_add<F>(acc, q + 5 * L, 3 * cq2);
+    lin_addp<F>(acc, q, 3 * cp0);
+    lin_addp<F>(acc, q + PL, 3 * cp1);
+    lin_addp<F>(acc, q + 2 * PL, 3 * cp2);
+    lin_addp<F>(acc, q + 3 * PL, 3 * cq0);
+    lin_addp<F>(acc, q + 4 * PL, 3 * cq1);
+    lin_addp<F>(acc, q + 5 * PL, 3 * cq2);
     lin_add<F>(acc, a + k * E2 + im * L, (k & 1) ? 2 : -2);
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
@@ -499,7 +540,7 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   uint32_t* prod = vw_smem + prod_o;
   using P = typename PairOf<C>::T;
   using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   const int lane = threadIdx.x;
   if (lane < 24) {
     const int k = lane >> 2, t = lane & 3;
@@ -514,16 +555,16 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     }
     // the chained product form (f29_mul_chain): measured 2.90 vs 3.38 us per
     // Frobenius against the latency-first form (profiles/r05_vw_ops_ab.json)
-    vw_st<C>(prod + lane * L, f29_mul_chain<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
+    vw_stp<C>(prod + lane * PL, f29_mul_chain<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
   }
   __syncthreads();
   if (lane < 12) {
     const int k = lane >> 1, im = lane & 1;
-    const uint32_t* q = prod + k * 4 * L;
+    const uint32_t* q = prod + k * 4 * PL;
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add<F>(acc, q + (im ? 2 : 0) * L, 1);
-    lin_add<F>(acc, q + (im ? 3 : 1) * L, im ? -1 : 1);
+    lin_addp<F>(acc, q + (im ? 2 : 0) * PL, 1);
+    lin_addp<F>(acc, q + (im ? 3 : 1) * PL, im ? -1 : 1);
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
   __syncthreads();
@@ -567,7 +608,7 @@ KZGX_TW void vw_inv(uint32_t dst_o, uint32_t a_o) {
 template <class C>
 KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t tb_o, uint32_t prod_o) {
   using F = typename C::Fp29;
-  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L;
+  constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t* prod = vw_smem + prod_o;
   uint32_t* tb = vw_smem + tb_o;
   uint32_t* sc = prod + 64 * L;  // scratch past the parts: F (2L), t (L), F^-1 (2L)
@@ -580,7 +621,7 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
     const int pr = lane / 3;
     const int x = pr == 0 ? 0 : pr == 1 ? 2 : pr == 2 ? 4 : pr == 3 ? 0 : pr == 4 ? 2 : 0;
     const int y = pr == 0 ? 0 : pr == 1 ? 4 : pr == 2 ? 4 : pr == 3 ? 2 : pr == 4 ? 2 : 4;
-    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + y * E2), lane % 3));
+    vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + y * E2), lane % 3));
   }
   __syncthreads();
   if (lane < 6) {  // A, B, C -> tb[1], tb[3], tb[5]
@@ -588,14 +629,14 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
     LinAcc<F> acc;
     lin_init<F>(acc);
     if (c == 0) {
-      lin_add_f2<F>(acc, prod + 0 * 3 * L, im, false, 1);
-      lin_add_f2<F>(acc, prod + 1 * 3 * L, im, true, -1);
+      lin_add_f2p<F, PL>(acc, prod + 0 * 3 * PL, im, false, 1);
+      lin_add_f2p<F, PL>(acc, prod + 1 * 3 * PL, im, true, -1);
     } else if (c == 1) {
-      lin_add_f2<F>(acc, prod + 2 * 3 * L, im, true, 1);
-      lin_add_f2<F>(acc, prod + 3 * 3 * L, im, false, -1);
+      lin_add_f2p<F, PL>(acc, prod + 2 * 3 * PL, im, true, 1);
+      lin_add_f2p<F, PL>(acc, prod + 3 * 3 * PL, im, false, -1);
     } else {
-      lin_add_f2<F>(acc, prod + 4 * 3 * L, im, false, 1);
-      lin_add_f2<F>(acc, prod + 5 * 3 * L, im, false, -1);
+      lin_add_f2p<F, PL>(acc, prod + 4 * 3 * PL, im, false, 1);
+      lin_add_f2p<F, PL>(acc, prod + 5 * 3 * PL, im, false, -1);
     }
     vw_st<C>(tb + (2 * c + 1) * E2 + im * L, lin_fin<F>(acc));
   }
@@ -604,29 +645,29 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
   if (lane < 9) {
     const int pr = lane / 3;
     const int x = pr == 0 ? 0 : pr == 1 ? 4 : 2;
-    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + (2 * pr + 1) * E2), lane % 3));
+    vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(tb + x * E2), vw_ld2<C>(tb + (2 * pr + 1) * E2), lane % 3));
   }
   __syncthreads();
   if (lane < 2) {
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add_f2<F>(acc, prod, lane, false, 1);
-    lin_add_f2<F>(acc, prod + 3 * L, lane, true, 1);
-    lin_add_f2<F>(acc, prod + 6 * L, lane, true, 1);
+    lin_add_f2p<F, PL>(acc, prod, lane, false, 1);
+    lin_add_f2p<F, PL>(acc, prod + 3 * PL, lane, true, 1);
+    lin_add_f2p<F, PL>(acc, prod + 6 * PL, lane, true, 1);
     vw_st<C>(sc + lane * L, lin_fin<F>(acc));
   }
   __syncthreads();
   // round C: t = F.re^2 + F.im^2
   if (lane < 2) {
     const F29<F> v = vw_ld<C>(sc + lane * L);
-    vw_st<C>(prod + lane * L, f29_mul<F>(v, v));
+    vw_stp<C>(prod + lane * PL, f29_mul<F>(v, v));
   }
   __syncthreads();
   if (lane == 0) {
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add<F>(acc, prod, 1);
-    lin_add<F>(acc, prod + L, 1);
+    lin_addp<F>(acc, prod, 1);
+    lin_addp<F>(acc, prod + PL, 1);
     vw_st<C>(sc + 2 * L, lin_fin<F>(acc));
   }
   __syncthreads();
@@ -641,7 +682,7 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
   // round E: A F^-1, B F^-1, C F^-1 -> tb = [A', 0, B', 0, C', 0]
   if (lane < 9) {
     const int pr = lane / 3;
-    vw_st<C>(prod + lane * L, vw_part<C>(vw_ld2<C>(tb + (2 * pr + 1) * E2), vw_ld2<C>(sc + 3 * L), lane % 3));
+    vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(tb + (2 * pr + 1) * E2), vw_ld2<C>(sc + 3 * L), lane % 3));
   }
   __syncthreads();
   if (lane < 12) {
@@ -650,7 +691,7 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
     if (!(k & 1)) {
       LinAcc<F> acc;
       lin_init<F>(acc);
-      lin_add_f2<F>(acc, prod + (k >> 1) * 3 * L, im, false, 1);
+      lin_add_f2p<F, PL>(acc, prod + (k >> 1) * 3 * PL, im, false, 1);
       v = lin_fin<F>(acc);
     }
     vw_st<C>(tb + k * E2 + im * L, v);
