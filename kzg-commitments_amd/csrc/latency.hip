@@ -23,6 +23,7 @@
 #define KZGX_FIELD_LATENCY
 #endif
 #include "coop.hpp"
+#include "msm_merge.hpp"
 #include "curve.hpp"
 #include "kzgx_internal.hpp"
 #include "kzgx_setup.hpp"
@@ -575,6 +576,23 @@ int big_reduce(int curve, const uint32_t* d_offsets, uint32_t nb, const uint32_t
                uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
   return curve == KZGX_CURVE_BN254 ? big_reduce_impl<BN254G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st)
                                    : big_reduce_impl<BLS12381G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st);
+}
+
+// the large-MSM path's segment merge with the XYZZ addition inlined
+// (k_msm_merge<C, true>): exact only with memory clauses off (DESIGN.md
+// section 7), which this translation unit is compiled with; msm.hip's batched
+// path keeps the called form
+int big_merge_inline(int curve, const uint32_t* heads, const uint32_t* tails, const uint32_t* tailk,
+                     const uint8_t* sstate, uint32_t smax, uint32_t nb, uint32_t nwg, uint32_t* bsum, uint32_t* ghead,
+                     uint32_t* gtail, uint32_t* gtailk, uint32_t* gflag, hipStream_t st) {
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL((k_msm_merge<BN254G1, true>), dim3(nwg, 1), dim3(ACC_WG), 0, st, heads, tails, tailk, sstate,
+                       smax, nb, nwg, bsum, ghead, gtail, gtailk, gflag);
+  else
+    hipLaunchKernelGGL((k_msm_merge<BLS12381G1, true>), dim3(nwg, 1), dim3(ACC_WG), 0, st, heads, tails, tailk,
+                       sstate, smax, nb, nwg, bsum, ghead, gtail, gtailk, gflag);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
 }
 
 int g1_fold_packed(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st) {

@@ -1465,6 +1465,11 @@ static int msm_single_chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uin
   return KZGX_OK;
 }
 
+// latency.hip: the segment merge with inlined additions (memory clauses off)
+int big_merge_inline(int curve, const uint32_t* heads, const uint32_t* tails, const uint32_t* tailk,
+                     const uint8_t* sstate, uint32_t smax, uint32_t nb, uint32_t nwg, uint32_t* bsum, uint32_t* ghead,
+                     uint32_t* gtail, uint32_t* gtailk, uint32_t* gflag, hipStream_t st);
+
 template <class C, int CB>
 static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
                         hipStream_t st) {
@@ -1555,8 +1560,13 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     ProfScope p(ctx, st, "msm_reduce");
     uint32_t* gh = ws.gpart;
     uint32_t* gt = ws.gpart + nwg2 * xyzz_words<C>();
-    hipLaunchKernelGGL(k_msm_merge<C>, dim3((unsigned)nwg2, 1), dim3(ACC_WG), 0, st, ws.heads, ws.tails, ws.tailk,
-                       ws.sstate, (uint32_t)smax2, NB, (uint32_t)nwg2, ws.bsum, gh, gt, ws.gmeta, ws.gmeta + nwg2);
+    static const bool merge_called = std::getenv("KZGX_BIG_MERGE_CALLED") != nullptr;  // A/B
+    if (merge_called)
+      hipLaunchKernelGGL(k_msm_merge<C>, dim3((unsigned)nwg2, 1), dim3(ACC_WG), 0, st, ws.heads, ws.tails, ws.tailk,
+                         ws.sstate, (uint32_t)smax2, NB, (uint32_t)nwg2, ws.bsum, gh, gt, ws.gmeta, ws.gmeta + nwg2);
+    else
+      KZGX_TRY(big_merge_inline(ctx->curve, ws.heads, ws.tails, ws.tailk, ws.sstate, (uint32_t)smax2, NB,
+                                (uint32_t)nwg2, ws.bsum, gh, gt, ws.gmeta, ws.gmeta + nwg2, st));
     hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg2 + 63) / 64), 1), dim3(64), 0, st, NB, (uint32_t)nwg2,
                        gh, gt, ws.gmeta, ws.gmeta + nwg2, ws.bsum);
     KZGX_TRY_HIP(hipGetLastError());
