@@ -93,7 +93,7 @@ def parse():
     ap.add_argument("--no-pippenger", action="store_true",
                     help="skip the secondary Pippenger (table-less, create_commit's default) leg")
     ap.add_argument("--no-table-curve", action="store_true",
-                    help="skip the throughput-vs-table-size leg (c = 10 .. 16 before the headline table)")
+                    help="skip the throughput-vs-table-size leg (c = 10 .. 16, after the headline table)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-call latency leg (benchmark/benchmark.cpp's timed regions)")
     ap.add_argument("--no-setup", action="store_true",
@@ -654,26 +654,6 @@ def main():
     if lat is not None:
         lat["pippenger"] = latency_leg(ctx, coeffs_h)
 
-    # throughput vs table size: what a re-linked create_commit gets at each
-    # HBM budget (trusted_setup::precompute_budget picks the widest window
-    # that fits); c = 0 is Pippenger, the table-less default
-    curve_pts = None
-    if fixed_bits and not args.no_table_curve:
-        curve_pts = [{"window_bits": 0, "gb": 0.0, "value": pip["value"] if pip else None}]
-        ctx.set_fixed_points_per_thread(args.fixed_ppt)
-        for cc in (10, 12, 14, 16):
-            if cc >= fixed_bits:
-                continue
-            tb = time.perf_counter()
-            built = set_fixed_with_fallback(kzgx, ctx, cc, n)
-            tb = time.perf_counter() - tb
-            if built != cc:
-                continue
-            ce, _, _ = timed_run(ctx, step, streams, 4, 1, world, dist, torch, dev)
-            curve_pts.append({"window_bits": cc, "gb": ctx.fixed_base_info()[2] / 1e9, "setup_s": tb,
-                              "value": units_all * 4 / ce})
-        ctx.set_fixed_base(0, 0)
-
     setup = None
     if rank == 0 and world == 1 and not args.no_setup and args.workload != "cfg3":
         try:
@@ -709,6 +689,37 @@ def main():
     bad = None
     if rank == 0:
         checked, ok, bad = check_step(curve, C, tau, args.workload, coeffs_h, zs_h, bufs, w64)
+
+    # ---- throughput vs table size: what a re-linked create_commit gets at
+    # each HBM budget (trusted_setup::precompute_budget picks the widest window
+    # that fits); c = 0 is Pippenger, the table-less default.  Run after the
+    # headline: the amdgpu driver wipes freed VRAM before it hands it out
+    # again (~30 GB/s, scripts/probe_alloc.hip, profiles/r06_probe_alloc.jsonl),
+    # so a table built right after a larger one was freed waits for that wipe;
+    # building the headline table first keeps its setup time the table's own.
+    # The curve's own setup_s values after the headline table's release
+    # include that wait. ----
+    curve_pts = None
+    if fixed_bits and not args.no_table_curve:
+        curve_pts = [{"window_bits": 0, "gb": 0.0, "value": pip["value"] if pip else None}]
+        if fb[0]:
+            curve_pts.append({"window_bits": fb[0], "gb": fb[2] / 1e9, "setup_s": t_setup,
+                              "value": units_all * args.steps / elapsed})
+        ctx.set_fixed_base(0, 0)
+        ctx.set_fixed_points_per_thread(args.fixed_ppt)
+        for cc in (10, 12, 14, 16):
+            if cc >= fixed_bits:
+                continue
+            tb = time.perf_counter()
+            built = set_fixed_with_fallback(kzgx, ctx, cc, n)
+            tb = time.perf_counter() - tb
+            if built != cc:
+                continue
+            ce, _, _ = timed_run(ctx, step, streams, 4, 1, world, dist, torch, dev)
+            curve_pts.append({"window_bits": cc, "gb": ctx.fixed_base_info()[2] / 1e9, "setup_s": tb,
+                              "value": units_all * 4 / ce})
+        ctx.set_fixed_base(0, 0)
+        curve_pts.sort(key=lambda e: e["window_bits"])
 
     # ---- CPU baseline (rank 0, N = 1 only) ----
     cpu = None
@@ -804,8 +815,6 @@ def main():
             mad_peak, mad_ghz = ctx.microbench_mad_u64_clock()
         except Exception as e:  # noqa: BLE001 -- reported, never fatal for the headline
             print("bench: VALU microbenchmarks unavailable: %s" % e, file=sys.stderr)
-        if curve_pts is not None and fb[0]:
-            curve_pts.append({"window_bits": fb[0], "gb": fb[2] / 1e9, "setup_s": t_setup, "value": value})
         L = 9 if curve == "BN254" else 14
         mpa = mads_per_mixed_add(L)
         isa = None
@@ -961,15 +970,15 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     coeffs_h = random_fr(rng, (n,), C.r)
     d_c = torch.from_numpy(coeffs_h[start:start + count].copy().view(np.int64)).to(dev)
     w64 = ctx.w64
-    # packed records (x || y canonical limbs, then an int64 infinity word):
-    # the partial MSM writes its record in place (the flag as the low 32
-    # bits of a zeroed int64), RCCL gathers the records into one tensor, and
-    # kzgx_g1_sum_packed_device folds them in one launch -- no stack / cast /
-    # cat between the phases (What's weak 4)
-    d_rec = torch.zeros((2 * w64 + 1,), dtype=torch.int64, device=dev)
+    # the partial MSM writes its record in place, RCCL gathers the records
+    # into one tensor and one launch folds them -- no stack / cast / cat
+    # between the phases (What's weak 4).  Round 6: the record
+    # each rank contributes is its partial left projective
+    # (one XYZZ point, kzgx_msm_g1_partial_device: no inversion on the rank);
+    # kzgx_g1_sum_partials_device adds the gathered records and inverts once,
+    # into the packed affine record (x || y || infinity word)
+    d_rec = torch.zeros((ctx.partial_record_words,), dtype=torch.int64, device=dev)  # all-zero: the identity
     d_res = torch.zeros((2 * w64 + 1,), dtype=torch.int64, device=dev)
-    if count == 0:  # an empty shard contributes the identity
-        d_rec[2 * w64] = 1
     stream = torch.cuda.Stream(device=dev)
 
     # Device-resident step: the partial MSM, the RCCL all-gather and the
@@ -977,12 +986,11 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     # inside a step.
     def partial(s0, cnt):
         if cnt:
-            ctx.msm_batch_device(d_c.data_ptr(), cnt, 1, cnt, d_rec.data_ptr(), d_rec.data_ptr() + 16 * w64,
-                                 stream.cuda_stream)
+            ctx.msm_partial_device(d_c.data_ptr(), cnt, d_rec.data_ptr(), stream.cuda_stream)
         return d_rec
 
     def fold(recs):
-        ctx.g1_sum_packed_device(recs.data_ptr(), recs.shape[0], d_res.data_ptr(), stream.cuda_stream)
+        ctx.g1_sum_partials_device(recs.data_ptr(), recs.shape[0], d_res.data_ptr(), stream.cuda_stream)
         return d_res
 
     # per-phase HIP events on the step's stream: start, partial MSM enqueued,
@@ -1028,7 +1036,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
             phase_tot[k] += t_k
             phase_min[k] = min(phase_min[k], t_k)
             phase_max[k] = max(phase_max[k], t_k)
-    nph = 3 if world > 1 else 1
+    nph = 3  # at world 1: the gather is empty and the fold is the one affine conversion
     my_phases = {names[k]: phase_tot[k] / max(1, len(marks)) for k in range(nph)}
     # per-step extremes, so a slow step (e.g. two ranks time-slicing one
     # device) shows in the record itself
@@ -1045,8 +1053,9 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
               "max_over_ranks": {k: max(r["phase_ms_per_step"].get(k, 0.0) for r in ranks) for k in my_phases},
               "min_max_over_steps_rank0": my_phase_range,
               "from": "HIP events on the step stream: partial_msm = this rank's shard MSM; all_gather = the "
-                      "%s all-gather of the packed partial records (until the stream may use them); fold = "
-                      "kzgx_g1_sum_packed_device of the gathered records" % dinfo.get("backend", "no")}
+                      "%s all-gather of the projective partial records (until the stream may use them); fold = "
+                      "kzgx_g1_sum_partials_device of the gathered records (the step's one inversion)"
+                      % dinfo.get("backend", "no")}
     if rank == 0:
         xys, infs = kzgx_dist.unpack_points(res.cpu().numpy(), w64)
         xy, inf = xys[0], bool(infs[0])
@@ -1061,7 +1070,8 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         unit_bytes = n * (P_b + 32) + P_b
         achieved = unit_bytes / (ms_per_step * 1e-3) / 1e9
         # the table-less window (msm.hip big_window_bits / big_min_points)
-        cbig = (16 if count >= (1 << 18) else 14) if count >= (1 << 16) else 0
+        cbig = int(os.environ.get("KZGX_BIG_WINDOW", "0")) or (16 if count >= (1 << 18) else 14)
+        cbig = cbig if count >= (1 << 16) else 0
         wins = ((C.r.bit_length() + fixed_bits - 1) // fixed_bits) if fixed_bits else \
             (257 + (cbig or args.window_bits) - 1) // (cbig or args.window_bits)
         madd_rate = n * wins / (ms_per_step * 1e-3)  # all ranks' mixed additions per second

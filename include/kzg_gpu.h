@@ -130,6 +130,16 @@ int kzgx_set_fixed_base_layout(kzgx_ctx* ctx, int layout);
  * installed. */
 int kzgx_set_default_table(kzgx_ctx* ctx, int c, size_t n_points);
 int kzgx_default_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_t* bytes);
+/* Contexts on one device whose SRS begins with the same n_points points (word
+ * for word) share one default table, counted by reference: the last context
+ * using it frees it.  *count / *bytes: the shared default tables live on
+ * `device` and their device bytes.  Extension, no reference counterpart. */
+int kzgx_shared_tables(int device, size_t* count, size_t* bytes);
+/* A freed default-size table block (1-32 GB) is kept per device for the next
+ * table build, since the driver wipes released VRAM before reuse (DESIGN.md
+ * section 3, "SRS").  It is released when the last context of the device is
+ * destroyed, before any allocation it cannot serve, or by this call. */
+int kzgx_release_cached_memory(int device);
 /* layout of the built table: *point_major = 1 (M[i][w][j]) or 0 (M[w][i][j]) */
 int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major);
 /* built table: window bits (0 = none), points covered, device bytes */
@@ -242,6 +252,17 @@ int kzgx_g1_sum_device(kzgx_ctx* ctx, const void* d_xy, const void* d_inf, size_
  * (strided sums, a shuffle tree, a wave-uniform inversion).  Device
  * pointers; stream as kzgx_msm_g1_batch_device. */
 int kzgx_g1_sum_packed_device(kzgx_ctx* ctx, const void* d_records, size_t count, void* d_out_record, void* stream);
+/* Projective partials (round 6): the sharded commitment's per-rank MSM left
+ * as one XYZZ point (X, Y, ZZ, ZZZ in the library's radix-2^29 Montgomery
+ * limbs; ZZ = 0 is infinity) -- an exchange format between ranks running this
+ * library, kzgx_partial_record_words(curve) uint64 words (BN254 18,
+ * BLS12-381 28) -- so no rank inverts; kzgx_g1_sum_partials_device adds
+ * count such records and converts the sum once, into one packed affine
+ * record (as kzgx_g1_sum_packed_device).  Device pointers; stream as
+ * kzgx_msm_g1_batch_device.  n = 0 gives the identity record. */
+int kzgx_partial_record_words(int curve);
+int kzgx_msm_g1_partial_device(kzgx_ctx* ctx, const void* d_scalars, size_t n, void* d_out_record, void* stream);
+int kzgx_g1_sum_partials_device(kzgx_ctx* ctx, const void* d_records, size_t count, void* d_out_record, void* stream);
 /* One commitment sharded over several contexts, typically one per GPU (the
  * one-process form of SURVEY 8e's sharded commit; bench.py's configs[4] runs
  * the one-process-per-GPU form over RCCL).  Context k holds the SRS slice
@@ -249,8 +270,8 @@ int kzgx_g1_sum_packed_device(kzgx_ctx* ctx, const void* d_records, size_t count
  * kzgx_load_srs_g1); the slices must be contiguous from 0 (starts[k + 1] ==
  * starts[k] + |SRS_k|, else KZGX_ERR_ARG) and cover n (else
  * KZGX_ERR_DEGREE).  Every context runs the partial MSM of its slice of
- * scalars[0..n) on its own stream, concurrently; the partial points are then
- * folded exactly on ctxs[0] (affine result, bit-exact with one MSM). */
+ * scalars[0..n) on its own stream, concurrently; the projective partials are
+ * then folded exactly on ctxs[0] (affine result, bit-exact with one MSM). */
 int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
                         size_t n, uint64_t* out_xy, int* out_is_inf);
 

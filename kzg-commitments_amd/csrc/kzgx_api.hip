@@ -37,6 +37,10 @@ struct kzgx_ctx {
   uint32_t* d_g2tab = nullptr;
   size_t g2tab_b = 0;
   size_t g2tab_n = 0;  // points covered; 0 = stale
+  // the table's build runs on a side stream at the end of a setup; calls
+  // that read it wait on g2tab_ev on the device (g2_table)
+  hipStream_t side = nullptr;
+  hipEvent_t g2tab_ev = nullptr;
   // pinned, device-mapped host staging for the host-pointer entry points
   // (kzgx_msm_g1_batch, kzgx_prove_single_batch): inputs are copied into it
   // and read by the kernels in place (small) or DMA'd from it (large); the
@@ -55,10 +59,14 @@ int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? KZGX_ERR_OOM : KZ
 // table freed (a context destroyed) is kept for the next context's table of
 // (about) the same size.  A trusted_setup per degree (the reference
 // benchmark, benchmark/benchmark.cpp:19-38) otherwise frees and re-allocates
-// an 11.8 GB default table each time, and one such hipMalloc in a few took
-// 5.3-5.8 s (profiles/r05_kzg_bench_cpp.txt: the 512-term setup; the bench's
-// setup leg).  The block is released before any allocation it cannot serve
-// and on any allocation failure; KZGX_NO_TABLE_CACHE=1 turns the cache off.
+// an 11.8 GB default table each time.  Why that matters: the amdgpu driver
+// wipes released VRAM before it hands it out again, at ~30 GB/s, and a
+// hipMalloc that lands on freed memory waits for that wipe (137 GB freed ->
+// the next large hipMalloc 4.1-4.9 s; 0.3 ms on clean memory;
+// scripts/probe_alloc.hip, profiles/r06_probe_alloc.jsonl).  The block is
+// released before any allocation it cannot serve, on any allocation failure,
+// when the last context of its device is destroyed, and by
+// kzgx_release_cached_memory; KZGX_NO_TABLE_CACHE=1 turns the cache off.
 namespace {
 struct TableBlock {
   void* p = nullptr;
@@ -66,24 +74,53 @@ struct TableBlock {
 };
 std::mutex g_table_mu;
 TableBlock g_table_cache[64];
+int g_live_ctx[64];  // live contexts per device (guarded by g_table_mu)
 bool table_cache_off() {
   static const bool off = std::getenv("KZGX_NO_TABLE_CACHE") && std::getenv("KZGX_NO_TABLE_CACHE")[0] == '1';
   return off;
 }
-}  // namespace
-
-void table_cache_release() {
-  std::lock_guard<std::mutex> lk(g_table_mu);
+int current_device() {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : -1;
+}
+void cache_release_locked(int dev) {
   TableBlock& b = g_table_cache[dev];
   if (b.p) (void)hipFree(b.p);
   b = TableBlock{};
 }
+}  // namespace
+
+void table_cache_release() {
+  const int dev = current_device();
+  if (dev < 0) return;
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  cache_release_locked(dev);
+}
+
+// a context created (+1) or destroyed (-1) on `dev`; the last one to go
+// releases the device's cached block (nothing else would)
+void ctx_live_add(int dev, int delta) {
+  if (dev < 0 || dev >= 64) return;
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  g_live_ctx[dev] += delta;
+  if (g_live_ctx[dev] <= 0) {
+    g_live_ctx[dev] = 0;
+    cache_release_locked(dev);
+  }
+}
+
+// bytes held by the current device's cached block: memory a table build may
+// count as free (table_malloc reuses or releases the block)
+size_t table_cache_bytes() {
+  const int dev = current_device();
+  if (dev < 0) return 0;
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  return g_table_cache[dev].bytes;
+}
 
 hipError_t table_malloc(void** p, size_t bytes) {
-  int dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+  const int dev = current_device();
+  if (dev >= 0) {
     std::lock_guard<std::mutex> lk(g_table_mu);
     TableBlock& b = g_table_cache[dev];
     if (b.p && b.bytes >= bytes && b.bytes - bytes <= bytes / 4) {
@@ -91,28 +128,106 @@ hipError_t table_malloc(void** p, size_t bytes) {
       b = TableBlock{};
       return hipSuccess;
     }
-    if (b.p) (void)hipFree(b.p);  // never hold a block beside a new allocation
-    b = TableBlock{};
+    cache_release_locked(dev);  // never hold a block beside a new allocation
   }
   return hipMalloc(p, bytes);
 }
 
 void table_free(void* p, size_t bytes) {
   if (!p) return;
-  int dev = 0;
+  const int dev = current_device();
   // only default-table sizes (1-32 GB): an opt-in table of hundreds of GB is
-  // freed at once (freeing a cached 137 GB block right before a 258 GB
-  // hipMalloc made the c = 17 build take 4.8 s instead of 0.6 s)
-  if (table_cache_off() || bytes < ((size_t)1 << 30) || bytes > ((size_t)32 << 30) || hipGetDevice(&dev) != hipSuccess ||
-      dev < 0 || dev >= 64) {
+  // freed at once (a cached 137 GB block beside a 258 GB request would have
+  // to be released, and wiped, right before it)
+  if (table_cache_off() || bytes < ((size_t)1 << 30) || bytes > ((size_t)32 << 30) || dev < 0) {
     (void)hipFree(p);
     return;
   }
   std::lock_guard<std::mutex> lk(g_table_mu);
-  TableBlock& b = g_table_cache[dev];
-  if (b.p) (void)hipFree(b.p);
-  b.p = p;
-  b.bytes = bytes;
+  cache_release_locked(dev);
+  g_table_cache[dev].p = p;
+  g_table_cache[dev].bytes = bytes;
+}
+
+// Shared default tables: contexts on one
+// device whose SRS starts with the same points (compared word for word, not
+// by a hash) and that pick the same window share one default table, counted
+// by reference.  kzgx_msm_g1_sharded-style callers and repeated trusted
+// setups then hold one 11.8 GB table, not one per context.
+namespace {
+struct SharedTable {
+  int id = 0;
+  int device = 0, curve = 0;
+  std::vector<uint32_t> srs;  // the canonical SRS prefix the table was built from
+  FixedTable t;               // owner's view of the table (d, inf, c, W, n_t, ...)
+  int refs = 0;
+};
+std::vector<SharedTable> g_shared;  // guarded by g_table_mu
+int g_shared_next = 1;
+}  // namespace
+
+bool table_share_attach(int device, int curve, int c_req, const std::vector<uint32_t>& srs, FixedTable& ft) {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  for (auto& e : g_shared) {
+    if (e.device != device || e.curve != curve || (c_req > 0 && e.t.c != c_req) || e.srs != srs) continue;
+    const uint32_t ppt = ft.pts_per_thread;
+    const int c_keep = ft.c_req;
+    const size_t n_keep = ft.n_req;
+    const int layout_keep = ft.layout_req;
+    ft = e.t;
+    ft.pts_per_thread = ppt;
+    ft.c_req = c_keep;
+    ft.n_req = n_keep;
+    ft.layout_req = layout_keep;
+    ft.shared = e.id;
+    e.refs++;
+    return true;
+  }
+  return false;
+}
+
+void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, FixedTable& ft) {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  SharedTable e;
+  e.id = g_shared_next++;
+  e.device = device;
+  e.curve = curve;
+  e.srs = std::move(srs);
+  e.t = ft;
+  e.refs = 1;
+  ft.shared = e.id;
+  g_shared.push_back(std::move(e));
+}
+
+// drop ft's reference; the last one frees the table (into the block cache)
+void table_share_release(FixedTable& ft) {
+  void* d = nullptr;
+  uint8_t* inf = nullptr;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    for (size_t k = 0; k < g_shared.size(); k++) {
+      if (g_shared[k].id != ft.shared) continue;
+      if (--g_shared[k].refs == 0) {
+        d = g_shared[k].t.d;
+        inf = g_shared[k].t.inf;
+        bytes = g_shared[k].t.bytes;
+        g_shared.erase(g_shared.begin() + (long)k);
+      }
+      break;
+    }
+  }
+  if (d) table_free(d, bytes);
+  if (inf) (void)hipFree(inf);
+}
+
+void shared_tables_info(int device, size_t* count, size_t* bytes) {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  size_t c = 0, b = 0;
+  for (auto& e : g_shared)
+    if (e.device == device) c++, b += e.t.bytes;
+  *count = c;
+  *bytes = b;
 }
 
 int dev_alloc(Ctx* ctx, void** p, size_t bytes, size_t* cap) {
@@ -306,9 +421,11 @@ int kzgx_init_device(int curve, int device) {
   } sg{st, device};
   // every code object of the library, once (the first launch of any kernel
   // of a translation unit loads its whole object)
-  int (*const warm[])(hipStream_t) = {kzgx::warm_setup, kzgx::warm_msm,     kzgx::warm_msm_fixed,
-                                       kzgx::warm_poly,  kzgx::warm_srs,     kzgx::warm_pairing,
-                                       kzgx::warm_verify_wave, kzgx::warm_latency};
+  int (*const warm[])(hipStream_t) = {
+      kzgx::warm_setup,      kzgx::warm_msm,        kzgx::warm_msm_fixed,   kzgx::warm_poly,
+      kzgx::warm_srs,        kzgx::warm_pairing,    kzgx::warm_verify_wave, kzgx::warm_latency,
+      kzgx::warm_fixed_bn_a, kzgx::warm_fixed_bn_b, kzgx::warm_fixed_bn_c,  kzgx::warm_fixed_bn_d,
+      kzgx::warm_fixed_bls_a, kzgx::warm_fixed_bls_b, kzgx::warm_fixed_bls_c, kzgx::warm_fixed_bls_d};
   for (auto f : warm) KZGX_TRY(f(st));
   // the generator comb tables (per process, per device and curve)
   kzgx::GenTables g;
@@ -340,7 +457,23 @@ int kzgx_create(kzgx_ctx** out, int curve, int device) {
     delete ctx;
     return kzgx::hip_fail(e);
   }
+  kzgx::ctx_live_add(device, +1);
   *out = ctx;
+  return KZGX_OK;
+}
+
+int kzgx_release_cached_memory(int device) {
+  if (device < 0 || device >= 64) return KZGX_ERR_ARG;
+  int prev = 0;
+  KZGX_TRY_HIP(hipGetDevice(&prev));
+  KZGX_TRY_HIP(hipSetDevice(device));
+  kzgx::table_cache_release();
+  return hipSetDevice(prev) == hipSuccess ? KZGX_OK : KZGX_ERR_HIP;
+}
+
+int kzgx_shared_tables(int device, size_t* count, size_t* bytes) {
+  if (!count || !bytes || device < 0 || device >= 64) return KZGX_ERR_ARG;
+  kzgx::shared_tables_info(device, count, bytes);
   return KZGX_OK;
 }
 
@@ -348,10 +481,12 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->c.device);
   (void)hipStreamSynchronize(ctx->c.stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_table_small, c.d_table_big, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
-                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw, ctx->d_g2tab};
+                  c.d_poly_ws, c.d_poly_ws2, ctx->d_srs_canon, ctx->d_srs2_canon, c.d_g2_ws, ctx->d_vw, ctx->d_g2tab,
+                  c.d_lift};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   kzgx::fixed_free(&c);
@@ -367,6 +502,9 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   (void)hipStreamSynchronize(c.stream);
   stream_give(c.device, c.stream);
+  if (ctx->side) stream_give(c.device, ctx->side);  // drained before the frees above
+  if (ctx->g2tab_ev) (void)hipEventDestroy(ctx->g2tab_ev);
+  kzgx::ctx_live_add(c.device, -1);
   delete ctx;
 }
 
@@ -516,6 +654,7 @@ int kzgx_set_fixed_base_budget(kzgx_ctx* ctx, size_t budget_bytes, size_t n_poin
   kzgx::fixed_free(&ctx->c);  // the old table's memory counts as free
   size_t free_b = 0, total_b = 0;
   KZGX_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
+  free_b += kzgx::table_cache_bytes();  // reused or released by table_malloc
   const size_t margin = (size_t)4 << 30;
   const size_t avail = free_b > margin ? free_b - margin : 0;
   const size_t cap = budget_bytes < avail ? budget_bytes : avail;
@@ -922,6 +1061,31 @@ int kzgx_g1_sum_packed_device(kzgx_ctx* ctx, const void* d_records, size_t count
                               pick(ctx, stream));
 }
 
+int kzgx_partial_record_words(int curve) {
+  if (curve != KZGX_CURVE_BN254 && curve != KZGX_CURVE_BLS12381) return -1;
+  return (int)(kzgx::xyzz_record_words(curve) / 2);
+}
+
+int kzgx_msm_g1_partial_device(kzgx_ctx* ctx, const void* d_scalars, size_t n, void* d_out_record, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (!d_out_record || (n > 0 && !d_scalars)) return KZGX_ERR_ARG;
+  if (ctx->c.n_srs == 0) return KZGX_ERR_NO_SRS;
+  if (n > ctx->c.n_srs) return KZGX_ERR_DEGREE;
+  hipStream_t st = pick(ctx, stream);
+  if (n == 0) {  // the identity: ZZ = 0
+    KZGX_TRY_HIP(hipMemsetAsync(d_out_record, 0, kzgx::xyzz_record_words(ctx->c.curve) * 4, st));
+    return KZGX_OK;
+  }
+  return kzgx::msm_partial_xyzz(&ctx->c, (const uint32_t*)d_scalars, n, (uint32_t*)d_out_record, st);
+}
+
+int kzgx_g1_sum_partials_device(kzgx_ctx* ctx, const void* d_records, size_t count, void* d_out_record, void* stream) {
+  KZGX_TRY(activate(ctx));
+  if (!d_out_record || (count > 0 && !d_records) || count > 0xffffffu) return KZGX_ERR_ARG;
+  return kzgx::g1_fold_xyzz(ctx->c.curve, (const uint32_t*)d_records, count, (uint32_t*)d_out_record,
+                            pick(ctx, stream));
+}
+
 int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx, const uint64_t* scalars,
                         size_t n, uint64_t* out_xy, int* out_is_inf) {
   if (!ctxs || !starts || nctx == 0 || (n > 0 && !scalars) || !out_xy || !out_is_inf) return KZGX_ERR_ARG;
@@ -937,15 +1101,17 @@ int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx
   }
   if (starts[nctx - 1] + ctxs[nctx - 1]->c.n_srs < n) return KZGX_ERR_DEGREE;
   const size_t pb = point_words(ctxs[0]) * 4;
+  // projective partial records (round 6): no shard converts its partial to
+  // affine; the fold's one inversion is the step's only one
+  const size_t rb = kzgx::xyzz_record_words(ctxs[0]->c.curve) * 4;
   kzgx_ctx* c0 = ctxs[0];
-  // the fold's inputs live on ctxs[0]'s device: nctx partial points
-  // (all-zero = infinity: empty shards contribute nothing) + their flags
+  // the fold's inputs live on ctxs[0]'s device: nctx partial records
+  // (all-zero = infinity: empty shards contribute nothing)
   void *d_gather, *d_res;
   KZGX_TRY(activate(c0));
-  KZGX_TRY(stage(c0, 2, nctx * (pb + 4) + 16, &d_gather));
+  KZGX_TRY(stage(c0, 2, nctx * rb + 16, &d_gather));
   KZGX_TRY(stage(c0, 3, pb + 16, &d_res));
-  uint32_t* d_flags = (uint32_t*)((char*)d_gather + nctx * pb);
-  KZGX_TRY_HIP(hipMemsetAsync(d_gather, 0, nctx * (pb + 4), c0->c.stream));
+  KZGX_TRY_HIP(hipMemsetAsync(d_gather, 0, nctx * rb, c0->c.stream));
   hipEvent_t zeroed;
   KZGX_TRY_HIP(hipEventCreateWithFlags(&zeroed, hipEventDisableTiming));
   std::vector<hipEvent_t> done;
@@ -967,13 +1133,11 @@ int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx
     KZGX_TRY(activate(c));
     void *d_s, *d_o;
     KZGX_TRY(stage(c, 0, cnt[k] * 32, &d_s));
-    KZGX_TRY(stage(c, 1, pb + 16, &d_o));
+    KZGX_TRY(stage(c, 1, rb + 16, &d_o));
     KZGX_TRY_HIP(hipMemcpyAsync(d_s, scalars + starts[k] * 4, cnt[k] * 32, hipMemcpyHostToDevice, c->c.stream));
-    KZGX_TRY(kzgx::msm_batch(&c->c, (const uint32_t*)d_s, cnt[k], 1, cnt[k] * 8, (uint32_t*)d_o,
-                             (uint32_t*)((char*)d_o + pb), c->c.stream));
+    KZGX_TRY(kzgx::msm_partial_xyzz(&c->c, (const uint32_t*)d_s, cnt[k], (uint32_t*)d_o, c->c.stream));
     KZGX_TRY_HIP(hipStreamWaitEvent(c->c.stream, zeroed, 0));
-    KZGX_TRY_HIP(hipMemcpyPeerAsync((char*)d_gather + k * pb, c0->c.device, d_o, c->c.device, pb, c->c.stream));
-    KZGX_TRY_HIP(hipMemcpyPeerAsync(d_flags + k, c0->c.device, (char*)d_o + pb, c->c.device, 4, c->c.stream));
+    KZGX_TRY_HIP(hipMemcpyPeerAsync((char*)d_gather + k * rb, c0->c.device, d_o, c->c.device, rb, c->c.stream));
     hipEvent_t e;
     KZGX_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     done.push_back(e);
@@ -981,8 +1145,8 @@ int kzgx_msm_g1_sharded(kzgx_ctx* const* ctxs, const size_t* starts, size_t nctx
   }
   KZGX_TRY(activate(c0));
   for (auto e : done) KZGX_TRY_HIP(hipStreamWaitEvent(c0->c.stream, e, 0));
-  uint32_t* d_oi = (uint32_t*)((char*)d_res + pb);
-  KZGX_TRY(kzgx::g1_sum(&c0->c, (const uint32_t*)d_gather, d_flags, nctx, (uint32_t*)d_res, d_oi, c0->c.stream));
+  uint32_t* d_oi = (uint32_t*)((char*)d_res + pb);  // the packed record's infinity word
+  KZGX_TRY(kzgx::g1_fold_xyzz(c0->c.curve, (const uint32_t*)d_gather, nctx, (uint32_t*)d_res, c0->c.stream));
   uint32_t oi = 0;
   KZGX_TRY_HIP(hipMemcpyAsync(out_xy, d_res, pb, hipMemcpyDeviceToHost, c0->c.stream));
   KZGX_TRY_HIP(hipMemcpyAsync(&oi, d_oi, 4, hipMemcpyDeviceToHost, c0->c.stream));
@@ -996,6 +1160,9 @@ namespace {
 // the G2 SRS's windowed table for n points (rebuilt when the SRS changed or
 // more points are needed); nullptr (plain per-term path) if it cannot be had
 const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
+  // a build enqueued on the side stream (g2_table_async) completes before
+  // st reads the table -- or rewrites it below
+  if (ctx->g2tab_ev && hipStreamWaitEvent(st, ctx->g2tab_ev, 0) != hipSuccess) return nullptr;
   if (ctx->g2tab_n >= n) return ctx->d_g2tab;
   const size_t all = ctx->n_srs2;
   ctx->g2tab_n = 0;
@@ -1006,6 +1173,32 @@ const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
     return nullptr;
   ctx->g2tab_n = all;
   return ctx->d_g2tab;
+}
+
+// the table of the whole G2 SRS built off the critical path: enqueued on the
+// context's side stream (after the setup's own work on its stream) and left
+// running.  One thread per point chains 16 windows of 16 doublings and an Fp2
+// inversion each, ~4.3 ms whatever the SRS size (profiles/
+// r05_kernel_stats_kzg_bench_final.csv) -- time the reference benchmark's
+// first multi-proof verify paid.  A failure leaves the
+// table stale: the first verify then builds it itself.
+int g2_table_async(kzgx_ctx* ctx) {
+  const size_t all = ctx->n_srs2;
+  ctx->g2tab_n = 0;
+  if (!ctx->side) KZGX_TRY_HIP(stream_take(ctx->c.device, &ctx->side));
+  if (!ctx->g2tab_ev) KZGX_TRY_HIP(hipEventCreateWithFlags(&ctx->g2tab_ev, hipEventDisableTiming));
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_g2tab, kzgx::g2_table_bytes(ctx->c.curve, all), &ctx->g2tab_b));
+  // the SRS and the buffer come from the context stream's work
+  hipEvent_t ready = nullptr;
+  KZGX_TRY_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(ready, ctx->c.stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side, ready, 0);
+  (void)hipEventDestroy(ready);
+  KZGX_TRY_HIP(e);
+  KZGX_TRY(kzgx::g2_table_build(&ctx->c, ctx->d_srs2_canon, all, ctx->d_g2tab, ctx->side));
+  KZGX_TRY_HIP(hipEventRecord(ctx->g2tab_ev, ctx->side));
+  ctx->g2tab_n = all;
+  return KZGX_OK;
 }
 }  // namespace
 
@@ -1263,6 +1456,17 @@ int setup_finish(kzgx_ctx* ctx) {
   for (int s = 0; s < 4; s++) KZGX_TRY(stage(ctx, s, (size_t)256 << 10, &d));
   KZGX_TRY_HIP(hipStreamSynchronize(st));
   ctx->vw_ready = true;
+  // the multi-point verify's workspaces at the reference benchmark's largest
+  // opening count (4096 points, benchmark/benchmark.cpp:85-99), and its G2
+  // table, built on the side stream while the caller goes on
+  {
+    const size_t nv = std::min<size_t>(ctx->n_srs2 - 1, 4096);
+    const size_t p1 = point_words(ctx) * 4, fb = 6 * p1;
+    const size_t o_o = 3 * nv * 32 + (nv + 1) * 32 + 6 * p1 + 4 * 2 * p1 + 64;
+    KZGX_TRY(stage(ctx, 3, ((o_o + 2 * fb + 255) & ~(size_t)255) + kzgx::pair2_wave_scratch_bytes(ctx->c.curve), &d));
+    KZGX_TRY(kzgx::verify_ws_reserve(&ctx->c, nv));
+    if (g2_table_async(ctx) != KZGX_OK) ctx->g2tab_n = 0;
+  }
   // the single-call workspaces (quotient, latency partials, arrival
   // counters, Pippenger buffers): one zero proof at the largest default
   // degree and one at degree 128 size them

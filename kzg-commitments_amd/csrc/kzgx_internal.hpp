@@ -91,7 +91,20 @@ struct FixedTable {
   uint8_t* inf = nullptr;  // [n_t] infinite SRS points (skipped)
   bool any_inf = true;     // some flag of inf is set (else the kernels get no flags)
   uint32_t fin0 = UINT32_MAX;  // first finite point of the prefix (k_fixed_accum's identity terms)
+  int shared = 0;  // registry id of a shared default table (kzgx_api.hip), 0 = owned by this context
 };
+
+// per-device table memory (kzgx_api.hip): the cached block of the last freed
+// default-size table, and the registry of default tables shared by contexts
+// with the same device, curve, window and SRS prefix
+hipError_t table_malloc(void** p, size_t bytes);
+void table_free(void* p, size_t bytes);
+void table_cache_release();
+size_t table_cache_bytes();
+bool table_share_attach(int device, int curve, int c_req, const std::vector<uint32_t>& srs, FixedTable& ft);
+void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, FixedTable& ft);
+void table_share_release(FixedTable& ft);
+void shared_tables_info(int device, size_t* count, size_t* bytes);
 
 // optional per-kernel timing with HIP events on the launch stream
 struct ProfRec {
@@ -212,6 +225,8 @@ struct Ctx {
   size_t poly_ws2_b = 0;
   void* d_g2_ws = nullptr;  // G2 MSM terms (pairing.hip)
   size_t g2_ws_b = 0;
+  uint32_t* d_lift = nullptr;  // msm_partial_xyzz's affine result before the lift
+  size_t lift_b = 0;
   // staging for host-pointer entry points
   void* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t stage_b[4] = {0, 0, 0, 0};
@@ -270,6 +285,8 @@ int debug_latency(Ctx* ctx, int op, uint32_t iters, double* res);  // ns, core c
 int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
               uint32_t* d_out_inf, hipStream_t st);
+// one MSM as an XYZZ record, no affine conversion (msm.hip)
+int msm_partial_xyzz(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_rec, hipStream_t st);
 int gen_srs_points(Ctx* ctx, const uint32_t* tau_canon_host, size_t start, size_t n, uint32_t* d_out_canon,
                    hipStream_t st);
 int g1_validate(Ctx* ctx, const uint32_t* d_xy, uint32_t* d_ok, hipStream_t st);
@@ -286,6 +303,8 @@ int prove_range_poly(Ctx* ctx, const uint32_t* d_P, size_t n, const uint32_t* d_
                      size_t* nq, hipStream_t st);
 int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
                      hipStream_t st);
+int verify_ws_reserve(Ctx* ctx, size_t n);  // poly.hip: workspaces of an n-point verify_proof
+int g2_ws_reserve(Ctx* ctx, size_t n);      // pairing.hip: an n-point G2 MSM's workspace
 
 // verify path: G2 SRS, polyeval_G2, pairing (pairing.hip)
 int gen_srs_g2_points(Ctx* ctx, const uint32_t* d_tau, size_t start, size_t n, uint32_t* d_out, hipStream_t st);

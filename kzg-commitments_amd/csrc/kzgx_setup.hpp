@@ -22,6 +22,15 @@ int warm_srs(hipStream_t st);
 int warm_pairing(hipStream_t st);
 int warm_verify_wave(hipStream_t st);
 int warm_latency(hipStream_t st);
+// the fixed-base MSM's per-window objects (msm_fixed_inst.hip, one per group)
+int warm_fixed_bn_a(hipStream_t st);
+int warm_fixed_bn_b(hipStream_t st);
+int warm_fixed_bn_c(hipStream_t st);
+int warm_fixed_bn_d(hipStream_t st);
+int warm_fixed_bls_a(hipStream_t st);
+int warm_fixed_bls_b(hipStream_t st);
+int warm_fixed_bls_c(hipStream_t st);
+int warm_fixed_bls_d(hipStream_t st);
 
 // Per-process tables of the curve generators, one per (device, curve), built
 // once (kzgx_init_device, or the first setup that needs them) and kept until
@@ -60,6 +69,12 @@ int vtab_prepare(int curve, const uint32_t* d_g1_0, const uint32_t* g1_comb, uin
 // the sharded commitment's fold (latency.hip): count packed records
 // (x || y canonical words, then a 64-bit infinity word) summed into one
 int g1_fold_packed(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st);
+// the same over projective partial records (one XYZZ point, xyzz_record_words
+// words each: the partials stay projective, the fold inverts once), and the
+// lift of an affine point (+ flag) into such a record
+size_t xyzz_record_words(int curve);
+int g1_fold_xyzz(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st);
+int affine_to_xyzz(int curve, const uint32_t* d_xy, const uint32_t* d_inf, uint32_t* d_rec, hipStream_t st);
 
 // latency of one wave-wide Fp12 op of the verify path (verify_wave.hip
 // k_vw_bench; kzgx_debug_vw_bench)
@@ -67,15 +82,17 @@ int vw_bench(int curve, int op, uint32_t iters, double* ns_per_op, double* clk_p
 
 // the bucket reduction of one wide-window Pippenger MSM (latency.hip):
 // sum_k (k + 1) B_k over nb >= 4096 buckets (bsum, occupancy from offsets)
-// -> canonical affine out / out_inf; d_rt: big_reduce_rt_bytes of scratch
+// -> canonical affine out / out_inf, or (xyzz_out) the XYZZ sum itself;
+// d_rt: big_reduce_rt_bytes of scratch
 size_t big_reduce_rt_bytes(int curve, uint32_t nb);
 int big_reduce(int curve, const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
-               uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
+               uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out = nullptr);
 // the same from bucket-aligned segment partials (msm.hip k_big2_*): bucket k
 // owns part[seg_off[k] .. seg_off[k + 1]); s_ub bounds seg_off[nb]; *d_flag:
 // some bucket has more than 64 partials (pre-sum passes run); part is
 // overwritten
 int big_reduce_seg(int curve, const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
-                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
+                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st,
+                   uint32_t* xyzz_out = nullptr);
 
 }  // namespace kzgx

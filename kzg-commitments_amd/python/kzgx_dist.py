@@ -4,10 +4,12 @@ One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm).
 The points of Σ c_i [tau^i]G1 are split into contiguous ranges; every rank
 generates its own SRS slice [tau^(start+i)]G1 on its GPU and computes the
 partial MSM of its range.  EC addition is not an RCCL reduction operator, so
-the one exchange step is an all-gather of the N partial affine points
-(N x (2 W64 + 1) int64 words: a few hundred bytes over xGMI) followed by an
-exact fold on every rank.  The fold is order-independent after affine
-normalization, so every rank holds the bit-exact commitment.
+the one exchange step is an all-gather of the N partial points (a few hundred
+bytes over xGMI) followed by an exact fold on every rank.  The fold's affine
+result is order-independent, so every rank holds the bit-exact commitment.
+Since round 6 the device path exchanges projective partials (one XYZZ point,
+kzgx_partial_record_words int64 words): no rank inverts its partial, and the
+fold's single inversion is the step's only one.
 
 The partial-MSM and fold callables are injected so the same driver runs
 with the GPU (kzgx.Context) in bench.py and with the CPU oracle in the
@@ -67,21 +69,26 @@ def sharded_commit_tensor(n: int, world: int, rank: int, w64: int,
                           dist, torch, on_phase: Optional[Callable[[str], None]] = None) -> "object":
     """Device-resident form of sharded_commit (bench.py's configs[4] step).
 
-    partial_msm(start, count) -> this rank's packed record (2 W64 + 1 int64:
-    x || y || infinity word) as a tensor on the compute device, enqueued with
-    no host synchronisation; the records are all-gathered (RCCL over xGMI on
-    GPU, gloo on CPU) straight into one (world, 2 W64 + 1) tensor, and
-    fold(records) -> the packed sum (kzgx_g1_sum_packed_device on the GPU).
-    Nothing crosses to the host inside a step, and nothing is repacked
-    between the phases.  on_phase(name), if given, is called after each phase
-    is enqueued ("partial", "gather", "fold"), e.g. to record timing events
-    on the step's stream."""
+    partial_msm(start, count) -> this rank's partial record (a 1-D int64
+    tensor on the compute device: on the GPU one projective XYZZ point,
+    kzgx_msm_g1_partial_device), enqueued with no host synchronisation; the
+    records are all-gathered (RCCL over xGMI on GPU, gloo on CPU) straight
+    into one (world, record) tensor, and fold(records) -> the packed affine
+    sum (x || y || infinity word; kzgx_g1_sum_partials_device on the GPU).
+    The fold runs at every world size -- at world 1 it is the partial's
+    affine conversion.  Nothing crosses to the host inside a step, and
+    nothing is repacked between the phases.  on_phase(name), if given, is
+    called after each phase is enqueued ("partial", "gather", "fold"), e.g.
+    to record timing events on the step's stream."""
     mark = on_phase or (lambda _name: None)
     start, count = shard_range(n, world, rank)
     packed = partial_msm(start, count)
     mark("partial")
-    if world == 1:
-        return packed
+    if world == 1:  # nothing to gather: the fold is the partial's conversion
+        mark("gather")
+        res = fold(packed.reshape(1, -1))
+        mark("fold")
+        return res
     g = torch.empty((world, packed.shape[0]), dtype=packed.dtype, device=packed.device)
     backend = dist.get_backend() if hasattr(dist, "get_backend") else None
     if backend == "nccl" and hasattr(dist, "all_gather_into_tensor"):

@@ -10,7 +10,11 @@
 // includes one-time work (kernel code-object loads, workspace growth).
 // Prints the reference's table and one JSON line.
 //
-//   kzg_bench [--json-only]
+//   kzg_bench [--json-only] [--curve BN254|BLS12381]
+//
+// The reference builds this benchmark once per curve (benchmark_curves.sh:
+// 43-51 rebuilds it with each miracl curve config); here the curve is the
+// run-time argument of kzg::init.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -48,10 +52,30 @@ static double median_ms(F&& f, int reps = 9) {
 }
 
 int main(int argc, char** argv) {
-  const bool json_only = argc > 1 && std::string(argv[1]) == "--json-only";
-  kzg::init();
+  bool json_only = false;
+  int curve = KZGX_CURVE_BN254;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    if (a == "--json-only") {
+      json_only = true;
+    } else if (a == "--curve" && i + 1 < argc) {
+      const std::string c = argv[++i];
+      if (c == "BN254") curve = KZGX_CURVE_BN254;
+      else if (c == "BLS12381" || c == "BLS12-381") curve = KZGX_CURVE_BLS12381;
+      else {
+        std::fprintf(stderr, "kzg_bench: unknown curve %s (BN254 or BLS12381)\n", c.c_str());
+        return 2;
+      }
+    } else {
+      std::fprintf(stderr, "usage: kzg_bench [--json-only] [--curve BN254|BLS12381]\n");
+      return 2;
+    }
+  }
+  kzg::init(curve);
+  if (!json_only) std::printf("curve: %s\n", curve == KZGX_CURVE_BN254 ? "BN254" : "BLS12381");
   std::mt19937 gen(0x4B5A47);
-  std::string js = "{\"setup_ms\": {";
+  std::string js = std::string("{\"curve\": \"") + (curve == KZGX_CURVE_BN254 ? "BN254" : "BLS12381") +
+                   "\", \"setup_ms\": {";
   if (!json_only) std::cout << "=== Benchmarking Trusted Setup ===" << std::endl;
   for (int max_degree = 128; max_degree <= 4096; max_degree *= 2) {
     const double t = ms_of([&] { kzg::trusted_setup s(max_degree); });

@@ -196,3 +196,45 @@ def test_single_opening_quotient_one_workgroup(name, C):
                 assert pt(name, out[b], inf[b]) == K.commit_via_tau(C, tau, q), (n, b)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_default_table_shared_across_contexts(name, C):
+    """8 contexts over one SRS hold ONE default table,
+    each of their commits exact; a context over another SRS builds its own;
+    the last context to go frees it"""
+    import kzgx
+    tau = K.default_tau(C) + 4242  # an SRS no other test's context holds
+    n0, b0 = kzgx.shared_tables(0)
+    ctxs = []
+    try:
+        for _ in range(8):
+            ctx = kzgx.Context(name)
+            ctx.gen_srs(tau, 700)
+            ctxs.append(ctx)
+        c, npts, b = ctxs[0].default_table_info()
+        assert npts == 700 and c >= 7
+        assert kzgx.shared_tables(0) == (n0 + 1, b0 + b)
+        for k, ctx in enumerate(ctxs):
+            assert ctx.default_table_info() == (c, npts, b)
+            P = K.random_scalars(C, 129 + 70 * k, seed=8100 + k)
+            out, inf = ctx.msm(limbs(P))
+            assert pt(name, out, inf) == K.commit_via_tau(C, tau, P), k
+        other = kzgx.Context(name)
+        ctxs.append(other)
+        other.gen_srs(tau + 1, 700)
+        assert kzgx.shared_tables(0)[0] == n0 + 2
+        P = K.random_scalars(C, 400, seed=8200)
+        out, inf = other.msm(limbs(P))
+        assert pt(name, out, inf) == K.commit_via_tau(C, tau + 1, P)
+        # dropping all but one holder keeps the table; the survivor is exact
+        for ctx in ctxs[:7]:
+            ctx.close()
+        ctxs = ctxs[7:]
+        assert kzgx.shared_tables(0)[0] == n0 + 2
+        out, inf = ctxs[0].msm(limbs(P))
+        assert pt(name, out, inf) == K.commit_via_tau(C, tau, P)
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    assert kzgx.shared_tables(0) == (n0, b0)

@@ -114,3 +114,64 @@ def test_init_device_twice():
     import kzgx
     for curve in ("BN254", "BLS12381", "BN254"):
         assert kzgx.lib().kzgx_init_device(kzgx.CURVES[curve], 0) == 0
+
+
+@pytest.mark.parametrize("name,C", CURVES)
+def test_partial_records_fold(name, C):
+    """The sharded commitment's round-6 exchange: every shard's MSM left
+    projective (kzgx_msm_g1_partial_device: one XYZZ record, no inversion),
+    the records folded with one inversion (kzgx_g1_sum_partials_device) --
+    against [P(tau)]G1.  Shards on every MSM path: the wide-window Pippenger
+    (>= 2^16 points), the main fixed table's flattened kernel, the default
+    table's one-launch kernel (lifted affine result), and an empty shard."""
+    import torch
+    import kzgx
+    tau = K.default_tau(C)
+    w = 4 if C is K.BN254 else 6
+    sizes = [70001, 3000, 60000, 0]
+    starts = [0, 70001, 73001, 133001]
+    n = sum(sizes)
+    P = K.random_scalars(C, n, seed=9100)
+    P[5], P[70001 + 7] = 0, C.r - 1
+    ctxs = []
+    try:
+        for s0, m in zip(starts, sizes):
+            c = kzgx.Context(name)
+            ctxs.append(c)
+            if m:
+                c.gen_srs(tau, m, start=s0)
+        ctxs[2].set_default_table(0)
+        ctxs[2].set_fixed_base(8, 60000)  # the main table (15.7 GB): flattened few-MSM kernel
+        rw = ctxs[0].partial_record_words
+        assert rw == (18 if C is K.BN254 else 28)
+        recs = torch.full((len(sizes), rw), -1, dtype=torch.int64, device="cuda")
+        for k, (c, s0, m) in enumerate(zip(ctxs, starts, sizes)):
+            d_s = torch.from_numpy(limbs(P[s0:s0 + m]).view(np.int64).reshape(-1) if m else np.zeros(4, np.int64)).cuda()
+            if m:
+                c.msm_partial_device(d_s.data_ptr(), m, recs[k].data_ptr())
+            else:
+                ctxs[0].msm_partial_device(d_s.data_ptr(), 0, recs[k].data_ptr())
+            torch.cuda.synchronize()
+        d_out = torch.full((2 * w + 1,), -1, dtype=torch.int64, device="cuda")
+        ctxs[0].g1_sum_partials_device(recs.data_ptr(), len(sizes), d_out.data_ptr())
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy().view(np.uint64)
+        assert int(out[-1]) == 0
+        assert point(C, out[: 2 * w], False) == K.commit_via_tau(C, tau, P)
+        # each record alone is its shard's commitment (the fold of one record
+        # is its affine conversion); a record and its negation cancel
+        for k, (s0, m) in enumerate(zip(starts, sizes)):
+            ctxs[0].g1_sum_partials_device(recs[k].data_ptr(), 1, d_out.data_ptr())
+            torch.cuda.synchronize()
+            out = d_out.cpu().numpy().view(np.uint64)
+            exp = K.commit_via_tau(C, tau, [0] * s0 + P[s0:s0 + m]) if m else None
+            assert (None if out[-1] else point(C, out[: 2 * w], False)) == exp, k
+        neg = [(C.r - v) % C.r for v in P[70001:73001]]
+        d_s = torch.from_numpy(limbs(neg).view(np.int64).reshape(-1)).cuda()
+        ctxs[1].msm_partial_device(d_s.data_ptr(), 3000, recs[2].data_ptr())
+        ctxs[0].g1_sum_partials_device(recs[1:].data_ptr(), 2, d_out.data_ptr())  # records 1 and -1
+        torch.cuda.synchronize()
+        assert int(d_out.cpu().numpy()[-1]) == 1
+    finally:
+        for c in ctxs:
+            c.close()
