@@ -954,7 +954,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     ctx.gen_srs(tau, max(count, 1), start)
     # Default (round 5): no fixed-base table -- the shard's MSM runs on the
     # wide-window Pippenger path (msm.hip msm_big: c = 16 from 2^18 SRS
-    # points, 14 below; the window table is built with the SRS), which beats
+    # points, 15 below (BLS12-381: 16); the window table is built with the SRS), which beats
     # the c = 8 table over the whole SRS (2.2 vs 3.05 ms per 2^20 + 1 commit).
     # --fixed-bits N: a fixed-base table over the shard, the widest window
     # whose table fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB;
@@ -1070,7 +1070,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
         unit_bytes = n * (P_b + 32) + P_b
         achieved = unit_bytes / (ms_per_step * 1e-3) / 1e9
         # the table-less window (msm.hip big_window_bits / big_min_points)
-        cbig = int(os.environ.get("KZGX_BIG_WINDOW", "0")) or (16 if count >= (1 << 18) else 14)
+        cbig = int(os.environ.get("KZGX_BIG_WINDOW", "0")) or (16 if count >= (1 << 18) else 15)
         cbig = cbig if count >= (1 << 16) else 0
         wins = ((C.r.bit_length() + fixed_bits - 1) // fixed_bits) if fixed_bits else \
             (257 + (cbig or args.window_bits) - 1) // (cbig or args.window_bits)

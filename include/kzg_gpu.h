@@ -135,10 +135,10 @@ int kzgx_default_table_info(const kzgx_ctx* ctx, int* c, size_t* n_points, size_
  * using it frees it.  *count / *bytes: the shared default tables live on
  * `device` and their device bytes.  Extension, no reference counterpart. */
 int kzgx_shared_tables(int device, size_t* count, size_t* bytes);
-/* A freed default-size table block (1-32 GB) is kept per device for the next
- * table build, since the driver wipes released VRAM before reuse (DESIGN.md
- * section 3, "SRS").  It is released when the last context of the device is
- * destroyed, before any allocation it cannot serve, or by this call. */
+/* Freed table blocks of 64 MB .. 32 GB are kept per device (32 GB in all)
+ * for later table builds, since the driver wipes released VRAM before reuse
+ * ("SRS").  They are released when the last context of
+ * the device is destroyed, on an allocation failure, or by this call. */
 int kzgx_release_cached_memory(int device);
 /* layout of the built table: *point_major = 1 (M[i][w][j]) or 0 (M[w][i][j]) */
 int kzgx_fixed_base_layout(const kzgx_ctx* ctx, int* point_major);

@@ -5,6 +5,7 @@
 // kzgx_create fails with KZGX_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <mutex>
 
 #include <array>
@@ -19,6 +20,12 @@
 #include "curve_consts.h"
 #include "kzgx_internal.hpp"
 #include "kzgx_setup.hpp"
+
+// a generated G2 SRS of at most this many points gets its polyeval_G2 window
+// table at setup (kzgx_gen_srs_g2); larger ones on first use
+#ifndef KZGX_G2TAB_EAGER_MAX
+#define KZGX_G2TAB_EAGER_MAX 16385
+#endif
 
 struct kzgx_ctx {
   kzgx::Ctx c;
@@ -37,10 +44,7 @@ struct kzgx_ctx {
   uint32_t* d_g2tab = nullptr;
   size_t g2tab_b = 0;
   size_t g2tab_n = 0;  // points covered; 0 = stale
-  // the table's build runs on a side stream at the end of a setup; calls
-  // that read it wait on g2tab_ev on the device (g2_table)
-  hipStream_t side = nullptr;
-  hipEvent_t g2tab_ev = nullptr;
+
   // pinned, device-mapped host staging for the host-pointer entry points
   // (kzgx_msm_g1_batch, kzgx_prove_single_batch): inputs are copied into it
   // and read by the kernels in place (small) or DMA'd from it (large); the
@@ -55,25 +59,33 @@ namespace kzgx {
 
 int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? KZGX_ERR_OOM : KZGX_ERR_HIP; }
 
-// One cached table block per device: the last large fixed-base / default
-// table freed (a context destroyed) is kept for the next context's table of
-// (about) the same size.  A trusted_setup per degree (the reference
-// benchmark, benchmark/benchmark.cpp:19-38) otherwise frees and re-allocates
-// an 11.8 GB default table each time.  Why that matters: the amdgpu driver
-// wipes released VRAM before it hands it out again, at ~30 GB/s, and a
-// hipMalloc that lands on freed memory waits for that wipe (137 GB freed ->
-// the next large hipMalloc 4.1-4.9 s; 0.3 ms on clean memory;
-// scripts/probe_alloc.hip, profiles/r06_probe_alloc.jsonl).  The block is
-// released before any allocation it cannot serve, on any allocation failure,
-// when the last context of its device is destroyed, and by
-// kzgx_release_cached_memory; KZGX_NO_TABLE_CACHE=1 turns the cache off.
+// Freed table blocks are cached per device for later tables.  A
+// trusted_setup per degree (the reference benchmark,
+// benchmark/benchmark.cpp:19-38) otherwise frees one default table and
+// allocates the next.  Why that matters: the amdgpu driver wipes released
+// VRAM before it hands it out again, at ~30 GB/s, and work on a block that
+// lands on freed memory waits for that wipe (137 GB freed -> the next large
+// hipMalloc 4.1-4.9 s, 0.3 ms on clean memory; scripts/probe_alloc.hip,
+// profiles/r06_probe_alloc.jsonl; a 737 MB table freed before the next
+// setup's 1.5 GB one cost that setup ~30 ms, profiles/r06_kzg_bench_cpp_run2.txt).
+// So a freed block of 64 MB .. 32 GB is kept (up to 32 GB per device in all,
+// oldest evicted first), a request takes the smallest cached block that
+// fits it with at most 2x + 64 MB slack, and a request nothing fits gets a
+// fresh allocation beside the cached blocks -- freeing them first would put
+// it on memory that is being wiped.  The cache is released on an allocation
+// failure, when the last context of the device is destroyed, and by
+// kzgx_release_cached_memory; KZGX_NO_TABLE_CACHE=1 turns it off.
 namespace {
 struct TableBlock {
   void* p = nullptr;
   size_t bytes = 0;
 };
+constexpr size_t CACHE_MIN = (size_t)64 << 20;
+constexpr size_t CACHE_CAP = (size_t)32 << 30;
 std::mutex g_table_mu;
-TableBlock g_table_cache[64];
+std::vector<TableBlock> g_table_cache[64];  // oldest first
+size_t g_cache_bytes[64];
+std::map<void*, size_t> g_block_bytes;  // true size of each block table_malloc handed out
 int g_live_ctx[64];  // live contexts per device (guarded by g_table_mu)
 bool table_cache_off() {
   static const bool off = std::getenv("KZGX_NO_TABLE_CACHE") && std::getenv("KZGX_NO_TABLE_CACHE")[0] == '1';
@@ -84,9 +96,12 @@ int current_device() {
   return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : -1;
 }
 void cache_release_locked(int dev) {
-  TableBlock& b = g_table_cache[dev];
-  if (b.p) (void)hipFree(b.p);
-  b = TableBlock{};
+  for (auto& b : g_table_cache[dev]) {
+    g_block_bytes.erase(b.p);
+    (void)hipFree(b.p);
+  }
+  g_table_cache[dev].clear();
+  g_cache_bytes[dev] = 0;
 }
 }  // namespace
 
@@ -98,7 +113,7 @@ void table_cache_release() {
 }
 
 // a context created (+1) or destroyed (-1) on `dev`; the last one to go
-// releases the device's cached block (nothing else would)
+// releases the device's cached blocks (nothing else would)
 void ctx_live_add(int dev, int delta) {
   if (dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> lk(g_table_mu);
@@ -109,44 +124,68 @@ void ctx_live_add(int dev, int delta) {
   }
 }
 
-// bytes held by the current device's cached block: memory a table build may
-// count as free (table_malloc reuses or releases the block)
+// bytes held by the current device's cached blocks: memory a table build may
+// count as free (table_malloc reuses them or releases them on failure)
 size_t table_cache_bytes() {
   const int dev = current_device();
   if (dev < 0) return 0;
   std::lock_guard<std::mutex> lk(g_table_mu);
-  return g_table_cache[dev].bytes;
+  return g_cache_bytes[dev];
 }
 
 hipError_t table_malloc(void** p, size_t bytes) {
   const int dev = current_device();
   if (dev >= 0) {
     std::lock_guard<std::mutex> lk(g_table_mu);
-    TableBlock& b = g_table_cache[dev];
-    if (b.p && b.bytes >= bytes && b.bytes - bytes <= bytes / 4) {
-      *p = b.p;
-      b = TableBlock{};
+    auto& c = g_table_cache[dev];
+    int best = -1;
+    for (int k = 0; k < (int)c.size(); k++)
+      if (c[k].bytes >= bytes && c[k].bytes <= 2 * bytes + CACHE_MIN && (best < 0 || c[k].bytes < c[best].bytes))
+        best = k;
+    if (best >= 0) {
+      *p = c[best].p;
+      g_cache_bytes[dev] -= c[best].bytes;
+      c.erase(c.begin() + best);
       return hipSuccess;
     }
-    cache_release_locked(dev);  // never hold a block beside a new allocation
   }
-  return hipMalloc(p, bytes);
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory && dev >= 0) {  // the cached blocks may be what is missing
+    (void)hipGetLastError();
+    {
+      std::lock_guard<std::mutex> lk(g_table_mu);
+      cache_release_locked(dev);
+    }
+    e = hipMalloc(p, bytes);
+  }
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    g_block_bytes[*p] = bytes;
+  }
+  return e;
 }
 
 void table_free(void* p, size_t bytes) {
   if (!p) return;
   const int dev = current_device();
-  // only default-table sizes (1-32 GB): an opt-in table of hundreds of GB is
-  // freed at once (a cached 137 GB block beside a 258 GB request would have
-  // to be released, and wiped, right before it)
-  if (table_cache_off() || bytes < ((size_t)1 << 30) || bytes > ((size_t)32 << 30) || dev < 0) {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  const auto it = g_block_bytes.find(p);
+  if (it != g_block_bytes.end()) bytes = it->second;  // the block's own size (it may have served a smaller table)
+  // blocks of 64 MB .. 32 GB: an opt-in table of hundreds of GB is freed at once
+  if (table_cache_off() || bytes < CACHE_MIN || bytes > CACHE_CAP || dev < 0) {
+    if (it != g_block_bytes.end()) g_block_bytes.erase(it);
     (void)hipFree(p);
     return;
   }
-  std::lock_guard<std::mutex> lk(g_table_mu);
-  cache_release_locked(dev);
-  g_table_cache[dev].p = p;
-  g_table_cache[dev].bytes = bytes;
+  auto& c = g_table_cache[dev];
+  c.push_back(TableBlock{p, bytes});
+  g_cache_bytes[dev] += bytes;
+  while (g_cache_bytes[dev] > CACHE_CAP && !c.empty()) {  // oldest first
+    g_cache_bytes[dev] -= c.front().bytes;
+    g_block_bytes.erase(c.front().p);
+    (void)hipFree(c.front().p);
+    c.erase(c.begin());
+  }
 }
 
 // Shared default tables: contexts on one
@@ -219,6 +258,23 @@ void table_share_release(FixedTable& ft) {
   }
   if (d) table_free(d, bytes);
   if (inf) (void)hipFree(inf);
+}
+
+// a pinned host buffer of at least `words` words for the sharing key's
+// device-to-host copy (per thread, grow-only, kept for the process): a
+// pageable destination sends the copy through the runtime's staging path,
+// which now and then stalls ~16 ms (profiles/r06_kzg_bench_trace_setup.txt)
+uint32_t* pinned_words(size_t words) {
+  thread_local uint32_t* buf = nullptr;
+  thread_local size_t cap = 0;
+  if (words <= cap) return buf;
+  if (buf) (void)hipHostFree(buf);
+  buf = nullptr;
+  cap = 0;
+  const size_t want = std::max<size_t>(words, (size_t)1 << 17);
+  if (hipHostMalloc((void**)&buf, want * 4, hipHostMallocDefault) != hipSuccess) return buf = nullptr;
+  cap = want;
+  return buf;
 }
 
 void shared_tables_info(int device, size_t* count, size_t* bytes) {
@@ -430,6 +486,28 @@ int kzgx_init_device(int curve, int device) {
   // the generator comb tables (per process, per device and curve)
   kzgx::GenTables g;
   KZGX_TRY(kzgx::gen_tables_get(curve, device, st, &g));
+  // the default-table sharing key's pinned copy buffer (4097 BLS12-381 points)
+  uint32_t* pw = kzgx::pinned_words((size_t)4097 * 24);
+  if (!pw) return KZGX_ERR_OOM;
+  // every copy path once, each way, pinned and pageable, at sizes past the
+  // runtime's small-copy path: the first copy of a kind in a process pays a
+  // one-time engine setup -- measured 4.7-17 ms on the first 32 KB
+  // device-to-host copy, inside the third setup of the reference benchmark's
+  // sweep (profiles/r06_kzg_bench_trace_setup.txt)
+  {
+    const size_t wb = (size_t)4097 * 24 * 4;
+    void* d = nullptr;
+    KZGX_TRY_HIP(hipMalloc(&d, wb));
+    std::vector<uint8_t> pg(wb, 0);
+    hipError_t e = hipMemcpyAsync(d, pw, wb, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(pw, d, wb, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, pg.data(), wb, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(pg.data(), d, wb, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync((uint8_t*)d + wb / 2, d, wb / 2, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    KZGX_TRY_HIP(e);
+  }
   // the pinned-allocation path of the host-pointer calls
   void* h = nullptr;
   KZGX_TRY_HIP(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
@@ -481,7 +559,6 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->c.device);
   (void)hipStreamSynchronize(ctx->c.stream);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   (void)kzgx_prof_clear(ctx);
   Ctx& c = ctx->c;
   void* bufs[] = {c.d_table, c.d_table_small, c.d_table_big, c.d_inf, c.d_stage[0], c.d_stage[1], c.d_stage[2], c.d_stage[3],
@@ -502,8 +579,6 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   (void)hipStreamSynchronize(c.stream);
   stream_give(c.device, c.stream);
-  if (ctx->side) stream_give(c.device, ctx->side);  // drained before the frees above
-  if (ctx->g2tab_ev) (void)hipEventDestroy(ctx->g2tab_ev);
   kzgx::ctx_live_add(c.device, -1);
   delete ctx;
 }
@@ -1160,9 +1235,6 @@ namespace {
 // the G2 SRS's windowed table for n points (rebuilt when the SRS changed or
 // more points are needed); nullptr (plain per-term path) if it cannot be had
 const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
-  // a build enqueued on the side stream (g2_table_async) completes before
-  // st reads the table -- or rewrites it below
-  if (ctx->g2tab_ev && hipStreamWaitEvent(st, ctx->g2tab_ev, 0) != hipSuccess) return nullptr;
   if (ctx->g2tab_n >= n) return ctx->d_g2tab;
   const size_t all = ctx->n_srs2;
   ctx->g2tab_n = 0;
@@ -1175,31 +1247,6 @@ const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
   return ctx->d_g2tab;
 }
 
-// the table of the whole G2 SRS built off the critical path: enqueued on the
-// context's side stream (after the setup's own work on its stream) and left
-// running.  One thread per point chains 16 windows of 16 doublings and an Fp2
-// inversion each, ~4.3 ms whatever the SRS size (profiles/
-// r05_kernel_stats_kzg_bench_final.csv) -- time the reference benchmark's
-// first multi-proof verify paid.  A failure leaves the
-// table stale: the first verify then builds it itself.
-int g2_table_async(kzgx_ctx* ctx) {
-  const size_t all = ctx->n_srs2;
-  ctx->g2tab_n = 0;
-  if (!ctx->side) KZGX_TRY_HIP(stream_take(ctx->c.device, &ctx->side));
-  if (!ctx->g2tab_ev) KZGX_TRY_HIP(hipEventCreateWithFlags(&ctx->g2tab_ev, hipEventDisableTiming));
-  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_g2tab, kzgx::g2_table_bytes(ctx->c.curve, all), &ctx->g2tab_b));
-  // the SRS and the buffer come from the context stream's work
-  hipEvent_t ready = nullptr;
-  KZGX_TRY_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-  hipError_t e = hipEventRecord(ready, ctx->c.stream);
-  if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side, ready, 0);
-  (void)hipEventDestroy(ready);
-  KZGX_TRY_HIP(e);
-  KZGX_TRY(kzgx::g2_table_build(&ctx->c, ctx->d_srs2_canon, all, ctx->d_g2tab, ctx->side));
-  KZGX_TRY_HIP(hipEventRecord(ctx->g2tab_ev, ctx->side));
-  ctx->g2tab_n = all;
-  return KZGX_OK;
-}
 }  // namespace
 
 size_t kzgx_srs_g2_size(const kzgx_ctx* ctx) { return ctx ? ctx->n_srs2 : 0; }
@@ -1218,7 +1265,18 @@ int kzgx_gen_srs_g2(kzgx_ctx* ctx, const uint64_t* tau, size_t start, size_t n) 
   KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, ctx->c.stream, &g));
   KZGX_TRY(kzgx::gen_srs_g2_comb(ctx->c.curve, (const uint32_t*)d_tau, start, n, g.g2_comb, ctx->d_srs2_canon,
                                  ctx->c.stream));
+  // polyeval_G2's window table from the same comb (one comb evaluation per
+  // entry, ~1 ms at 4097 points) so no verify_proof(poly, 0, N) pays the
+  // 4.3-ms doubling chains of building it from the points (k_g2_tab, still
+  // the path of a loaded G2 SRS); large SRSs keep it for first use
+  const bool eager = n <= KZGX_G2TAB_EAGER_MAX;
+  if (eager) {
+    KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_g2tab, kzgx::g2_table_bytes(ctx->c.curve, n), &ctx->g2tab_b));
+    KZGX_TRY(kzgx::g2_table_comb(ctx->c.curve, (const uint32_t*)d_tau, start, n, g.g2_comb, ctx->d_g2tab,
+                                 ctx->c.stream));
+  }
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+  ctx->g2tab_n = eager ? n : 0;
   ctx->n_srs2 = n;
   return setup_finish(ctx);
 }
@@ -1457,15 +1515,13 @@ int setup_finish(kzgx_ctx* ctx) {
   KZGX_TRY_HIP(hipStreamSynchronize(st));
   ctx->vw_ready = true;
   // the multi-point verify's workspaces at the reference benchmark's largest
-  // opening count (4096 points, benchmark/benchmark.cpp:85-99), and its G2
-  // table, built on the side stream while the caller goes on
+  // opening count (4096 points, benchmark/benchmark.cpp:85-99)
   {
     const size_t nv = std::min<size_t>(ctx->n_srs2 - 1, 4096);
     const size_t p1 = point_words(ctx) * 4, fb = 6 * p1;
     const size_t o_o = 3 * nv * 32 + (nv + 1) * 32 + 6 * p1 + 4 * 2 * p1 + 64;
     KZGX_TRY(stage(ctx, 3, ((o_o + 2 * fb + 255) & ~(size_t)255) + kzgx::pair2_wave_scratch_bytes(ctx->c.curve), &d));
     KZGX_TRY(kzgx::verify_ws_reserve(&ctx->c, nv));
-    if (g2_table_async(ctx) != KZGX_OK) ctx->g2tab_n = 0;
   }
   // the single-call workspaces (quotient, latency partials, arrival
   // counters, Pippenger buffers): one zero proof at the largest default

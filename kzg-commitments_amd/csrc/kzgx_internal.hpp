@@ -105,6 +105,7 @@ bool table_share_attach(int device, int curve, int c_req, const std::vector<uint
 void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, FixedTable& ft);
 void table_share_release(FixedTable& ft);
 void shared_tables_info(int device, size_t* count, size_t* bytes);
+uint32_t* pinned_words(size_t words);  // per-thread pinned host scratch (grow-only)
 
 // optional per-kernel timing with HIP events on the launch stream
 struct ProfRec {

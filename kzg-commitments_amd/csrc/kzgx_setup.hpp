@@ -69,6 +69,12 @@ int vtab_prepare(int curve, const uint32_t* d_g1_0, const uint32_t* g1_comb, uin
 // the sharded commitment's fold (latency.hip): count packed records
 // (x || y canonical words, then a 64-bit infinity word) summed into one
 int g1_fold_packed(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st);
+// polyeval_G2's windowed table (pairing.hip k_g2_terms_w) of a generated G2
+// SRS [tau^(start+i)]G2, i < n: G2_TAB_WINDOWS entries per point from the
+// generator's comb (setup.hip k_g2_tab_comb)
+constexpr int G2_TAB_WINDOWS = 16;
+int g2_table_comb(int curve, const uint32_t* d_tau, size_t start, size_t n, const uint32_t* g2_comb, uint32_t* d_tab,
+                  hipStream_t st);
 // the same over projective partial records (one XYZZ point, xyzz_record_words
 // words each: the partials stay projective, the fold inverts once), and the
 // lift of an affine point (+ flag) into such a record

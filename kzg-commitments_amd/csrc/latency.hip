@@ -89,27 +89,32 @@ __global__ __launch_bounds__(64) void k_g1_fold_packed(const uint32_t* __restric
 // partial to affine -- the fold's one wave-uniform inversion is the only
 // one of the step.  Output: one packed affine record, as k_g1_fold_packed.
 template <class C>
+KZGX_DEV Xyzz<C> xyzz_shfl_down_w(const Xyzz<C>& p, int off);
+
+// Group-cooperative (coop.hpp: 8 lanes per addition, ~1/3 of a lone lane's
+// latency): group g sums records g, g + 8, ...; a 3-level tree over the
+// groups; the whole wave then converts group 0's sum (one wave-uniform
+// inversion).  For the 2-8 records of a sharded step the chain is three
+// cooperative additions and the inversion.
+template <class C>
 __global__ __launch_bounds__(64) void k_g1_fold_xyzz(const uint32_t* __restrict__ rec, uint32_t count,
                                                      uint32_t* __restrict__ out) {
   constexpr int N = C::Fp::N, L = C::Fp29::L;
   constexpr int XW = xyzz_words<C>();
-  const uint32_t lane = threadIdx.x;
-  Xyzz<C> acc = xyzz_inf<C>();
-  for (uint32_t k = lane; k < count; k += 64) acc = xyzz_add_impl<C>(acc, xyzz_load<C>(rec + (size_t)k * XW));
-  for (int off = 32; off >= 1; off >>= 1) {
-    if (count <= (uint32_t)off) continue;  // uniform: no lane >= off holds a record
-    Xyzz<C> o;
-#pragma unroll
-    for (int k = 0; k < L; k++) {
-      o.X.v[k] = __shfl_xor(acc.X.v[k], off, 64);
-      o.Y.v[k] = __shfl_xor(acc.Y.v[k], off, 64);
-      o.ZZ.v[k] = __shfl_xor(acc.ZZ.v[k], off, 64);
-      o.ZZZ.v[k] = __shfl_xor(acc.ZZZ.v[k], off, 64);
-    }
-    acc = xyzz_add_impl<C>(acc, o);
+  __shared__ uint32_t sc[8 * COOP_SLOTS * L];
+  const uint32_t lane = threadIdx.x, g = lane >> 3;
+  const int j = (int)(lane & 7);
+  uint32_t* my = sc + g * COOP_SLOTS * L;
+  Xyzz<C> acc = g < count ? xyzz_load<C>(rec + (size_t)g * XW) : xyzz_inf<C>();
+  for (uint32_t k = g + 8; k < count; k += 8) acc = coop_add<C>(acc, xyzz_load<C>(rec + (size_t)k * XW), my, j);
+#pragma unroll 1
+  for (uint32_t o = 4; o >= 1; o >>= 1) {
+    if (count <= o) continue;  // uniform: groups >= o hold only the identity
+    const Xyzz<C> x = xyzz_shfl_down_w<C>(acc, (int)(8 * o));
+    if (g < o) acc = coop_add<C>(acc, x, my, j);
   }
   Affine<C> a;
-  const bool fin = xyzz_to_affine_impl<C, true>(acc, a);
+  const bool fin = xyzz_to_affine_impl<C, true>(acc, a);  // lane 0's value (group 0: the sum)
   if (lane == 0) {
     affine_to_canonical<C>(out, a, fin);
     out[2 * N] = fin ? 0u : 1u;

@@ -1235,11 +1235,21 @@ static size_t big_min_points() {
   return v ? v : ~(size_t)0;
 }
 // its window for an SRS of n points: fewer additions per point (n W) against
-// a deeper bucket reduction (log2 of 2^(c-1) buckets); KZGX_BIG_WINDOW pins it
-static int big_window_bits(size_t n) {
+// a deeper bucket reduction (log2 of 2^(c-1) buckets) -- and a top window
+// that spreads.  Scalars are uniform below r (BN254 2^253.6, BLS12-381
+// 2^254.9), so the top window's digit takes only the values r's top bits
+// allow: at BN254 c = 14 (window 18 = bits 252..) a handful, which drops
+// ~n/2 entries into 4 buckets (their pre-sum passes made a 131 073-point MSM
+// 1.19 ms); c = 15 (bits 240..254, up to 12 388) and 16 (bits 240..255) spread
+// them, and for BLS12-381 only c = 16 keeps the top digit below 2^(c-1) (no
+// carry into a near-empty extra window).  Measured at 131 073 points,
+// uniform scalars: c = 13 / 14 / 15 / 16 -> 0.79 / 1.19 / 0.65-0.68 /
+// 0.76-0.83 ms (profiles/r06_shard8_window_ab.jsonl).  KZGX_BIG_WINDOW pins it.
+static int big_window_bits(size_t n, int curve) {
   static const int pin = std::getenv("KZGX_BIG_WINDOW") ? std::atoi(std::getenv("KZGX_BIG_WINDOW")) : 0;
   if (pin >= 12 && pin <= 16) return pin;
-  return n >= ((size_t)1 << 18) ? 16 : 14;
+  if (curve != KZGX_CURVE_BN254) return 16;
+  return n >= ((size_t)1 << 18) ? 16 : 15;
 }
 
 template <class C>
@@ -1261,7 +1271,7 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   // Montgomery SRS, window 0 of the main table)
   ctx->c_big = 0;
   if (n >= big_min_points()) {
-    const int cb = big_window_bits(n);
+    const int cb = big_window_bits(n, ctx->curve);
     const int WB = (257 + cb - 1) / cb;
     KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_big, (size_t)WB * n * pw, &ctx->table_big_bytes));
     KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_big, ctx->d_table, n * pw, hipMemcpyDeviceToDevice, ctx->stream));

@@ -307,10 +307,14 @@ static int fixed_build_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) 
   if (ft.c_req == 0 || ft.n_req == 0) return KZGX_OK;
   fixed_free_table(ft);  // its memory counts as free for the choice
   const size_t n = ft.n_req < n_srs ? ft.n_req : n_srs;
-  // the SRS prefix, word for word, is the sharing key
-  std::vector<uint32_t> key((size_t)n * 2 * ctx->base_words());
-  KZGX_TRY_HIP(hipMemcpyAsync(key.data(), d_canon, key.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+  // the SRS prefix, word for word, is the sharing key (copied through pinned
+  // memory: a pageable destination now and then stalls the copy ~16 ms)
+  const size_t kw = (size_t)n * 2 * ctx->base_words();
+  uint32_t* pin = pinned_words(kw);
+  if (!pin) return KZGX_ERR_OOM;
+  KZGX_TRY_HIP(hipMemcpyAsync(pin, d_canon, kw * 4, hipMemcpyDeviceToHost, ctx->stream));
   KZGX_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<uint32_t> key(pin, pin + kw);
   if (table_share_attach(ctx->device, ctx->curve, ft.c_req, key, ft)) return KZGX_OK;
   auto build = [&](int c) {
     const int keep = ft.c_req;

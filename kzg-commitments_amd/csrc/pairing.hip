@@ -296,6 +296,7 @@ __global__ __launch_bounds__(64) void k_g2_sum(const G2J<C>* __restrict__ terms,
 // additions instead of a 256-bit double-and-add, and the n 16 partial
 // points are folded 8:1 per pass, then by a one-workgroup tree.
 constexpr int G2_TAB_W = 16;
+static_assert(G2_TAB_W == G2_TAB_WINDOWS, "setup.hip k_g2_tab_comb builds the same table");
 
 template <class C>
 __global__ __launch_bounds__(64) void k_g2_tab(const uint32_t* __restrict__ srs2, uint32_t n,

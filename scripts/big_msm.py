@@ -22,10 +22,14 @@ import corc  # noqa: E402  (checker only: Horner of P at tau)
 
 C = K.BN254
 tau = K.default_tau(C)
-rng = np.random.default_rng(5)
+sys.path.insert(0, ROOT)
+from bench import random_fr  # noqa: E402
+
 NMAX = (1 << 20) + 1
-P = rng.integers(0, 2**63, size=(NMAX, 4), dtype=np.uint64)
-P[:, 3] &= np.uint64((1 << 59) - 1)
+# uniform in [0, r) (round 6; round 5 drew 251-bit scalars, whose top window
+# is empty -- real scalars put up to r's top bits there, and a window whose
+# top digit takes few values concentrates entries in a few buckets)
+P = random_fr(np.random.default_rng(5), (NMAX,), C.r)
 corc.build()
 
 
@@ -55,7 +59,8 @@ def run(srs_n, n):
         exp = K.scalar_mul(C, (C.gx, C.gy), corc.poly_eval("BN254", P[:n], tau))
         rec = {"srs_points": srs_n, "n": n, "median_ms": float(np.median(ts)), "min_ms": float(min(ts)),
                "per_s": 1e3 / float(np.median(ts)), "checked": got == exp,
-               "path": "chunked c=12" if os.environ.get("KZGX_BIG_MIN") == "0" else "wide-window"}
+               "path": "chunked c=12" if os.environ.get("KZGX_BIG_MIN") == "0" else "wide-window",
+               "big_window": os.environ.get("KZGX_BIG_WINDOW", "auto")}
         print(json.dumps(rec), flush=True)
         assert got == exp
     finally:

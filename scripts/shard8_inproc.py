@@ -28,9 +28,10 @@ world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 C = K.BN254
 tau = K.default_tau(C)
 n = (1 << 20) + 1
-rng = np.random.default_rng(0x4B5A47)
-P = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
-P[:, 3] &= np.uint64((1 << 60) - 1)  # < r
+sys.path.insert(0, ROOT)
+from bench import random_fr  # noqa: E402  (uniform in [0, r): the bench's cfg5 scalars)
+
+P = random_fr(np.random.default_rng(0x4B5A47), (n,), C.r)
 corc.build()
 
 

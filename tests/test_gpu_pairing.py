@@ -143,6 +143,12 @@ def test_msm_g2_windowed_edges(name, C, ctxs):
     sc = [sum(1 << (16 * w + (w % 16)) for w in range(15)), (1 << 16) - 1, 1 << 240, 0, C.r - 2, 65536]
     out, inf = ctx.msm_g2(scalars(sc))
     assert g2_from_row(C, out, inf) == PR.polyeval_g2(C, srs2, sc)
+    # the same SRS loaded (no tau): the table is built from the points on
+    # first use (k_g2_tab) instead of from the generator's comb at setup
+    # (k_g2_tab_comb); same sums
+    ctx.load_srs_g2(ctx.get_srs_g2(n))
+    out2, inf2 = ctx.msm_g2(scalars(sc))
+    assert np.array_equal(out2, out) and inf2 == inf
 
 
 @pytest.mark.parametrize("name,C", CURVES)

@@ -169,6 +169,7 @@ def test_partial_records_fold(name, C):
         neg = [(C.r - v) % C.r for v in P[70001:73001]]
         d_s = torch.from_numpy(limbs(neg).view(np.int64).reshape(-1)).cuda()
         ctxs[1].msm_partial_device(d_s.data_ptr(), 3000, recs[2].data_ptr())
+        torch.cuda.synchronize()  # ctxs[1]'s stream wrote it; the fold runs on ctxs[0]'s
         ctxs[0].g1_sum_partials_device(recs[1:].data_ptr(), 2, d_out.data_ptr())  # records 1 and -1
         torch.cuda.synchronize()
         assert int(d_out.cpu().numpy()[-1]) == 1
