@@ -66,9 +66,7 @@ int hip_fail(hipError_t e) { return e == hipErrorOutOfMemory ? KZGX_ERR_OOM : KZ
 // VRAM before it hands it out again, at ~30 GB/s, and work on a block that
 // lands on freed memory waits for that wipe (137 GB freed -> the next large
 // hipMalloc 4.1-4.9 s, 0.3 ms on clean memory; scripts/probe_alloc.hip,
-// profiles/r06_probe_alloc.jsonl; a 737 MB table freed before the next
-// setup's 1.5 GB one cost that setup ~30 ms, profiles/r06_kzg_bench_cpp_run2.txt).
-// So a freed block of 64 MB .. 32 GB is kept (up to 32 GB per device in all,
+// profiles/r06_probe_alloc.jsonl).  So a freed block of 64 MB .. 32 GB is kept (up to 32 GB per device in all,
 // oldest evicted first), a request takes the smallest cached block that
 // fits it with at most 2x + 64 MB slack, and a request nothing fits gets a
 // fresh allocation beside the cached blocks -- freeing them first would put
@@ -197,18 +195,47 @@ namespace {
 struct SharedTable {
   int id = 0;
   int device = 0, curve = 0;
-  std::vector<uint32_t> srs;  // the canonical SRS prefix the table was built from
-  FixedTable t;               // owner's view of the table (d, inf, c, W, n_t, ...)
+  uint32_t* d_key = nullptr;  // device copy of the canonical SRS prefix the table was built from
+  size_t key_words = 0;
+  FixedTable t;  // owner's view of the table (d, inf, c, W, n_t, ...)
   int refs = 0;
 };
 std::vector<SharedTable> g_shared;  // guarded by g_table_mu
 int g_shared_next = 1;
+
+// *differ = (a[0..words) != b[0..words)), both on the device, compared by a
+// kernel that stores into a mapped host word: the setup path makes no
+// device-to-host copy (a 32 KB one stalled 6-18 ms now and then inside the
+// reference benchmark's 512-term setup, profiles/r06_kzg_bench_trace_setup.txt)
+__global__ void k_words_differ(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, size_t words,
+                               volatile uint32_t* __restrict__ flag) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += (size_t)gridDim.x * blockDim.x)
+    if (a[k] != b[k]) *flag = 1u;  // every writer stores the same value
+}
+int words_differ(const uint32_t* a, const uint32_t* b, size_t words, hipStream_t st, bool* differ) {
+  thread_local uint32_t* h_flag = nullptr;  // mapped pinned word, kept for the thread
+  thread_local uint32_t* d_flag = nullptr;
+  if (!h_flag) {
+    KZGX_TRY_HIP(hipHostMalloc((void**)&h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    KZGX_TRY_HIP(hipHostGetDevicePointer((void**)&d_flag, h_flag, 0));
+  }
+  *(volatile uint32_t*)h_flag = 0u;
+  const unsigned blocks = (unsigned)std::min<size_t>((words + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_words_differ, dim3(blocks ? blocks : 1), dim3(256), 0, st, a, b, words, d_flag);
+  KZGX_TRY_HIP(hipGetLastError());
+  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  *differ = *(volatile uint32_t*)h_flag != 0u;
+  return KZGX_OK;
+}
 }  // namespace
 
-bool table_share_attach(int device, int curve, int c_req, const std::vector<uint32_t>& srs, FixedTable& ft) {
+bool table_share_attach(int device, int curve, int c_req, const uint32_t* d_canon, size_t key_words, hipStream_t st,
+                        FixedTable& ft) {
   std::lock_guard<std::mutex> lk(g_table_mu);
   for (auto& e : g_shared) {
-    if (e.device != device || e.curve != curve || (c_req > 0 && e.t.c != c_req) || e.srs != srs) continue;
+    if (e.device != device || e.curve != curve || (c_req > 0 && e.t.c != c_req) || e.key_words != key_words) continue;
+    bool differ = true;
+    if (words_differ(e.d_key, d_canon, key_words, st, &differ) != KZGX_OK || differ) continue;
     const uint32_t ppt = ft.pts_per_thread;
     const int c_keep = ft.c_req;
     const size_t n_keep = ft.n_req;
@@ -225,13 +252,27 @@ bool table_share_attach(int device, int curve, int c_req, const std::vector<uint
   return false;
 }
 
-void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, FixedTable& ft) {
+// ft (just built from d_canon's first key_words words) becomes shareable; a
+// failure to keep the key just leaves it unshared
+void table_share_register(int device, int curve, const uint32_t* d_canon, size_t key_words, hipStream_t st,
+                          FixedTable& ft) {
+  uint32_t* d_key = nullptr;
+  if (hipMalloc((void**)&d_key, key_words * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  if (hipMemcpyAsync(d_key, d_canon, key_words * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    (void)hipFree(d_key);
+    return;
+  }
   std::lock_guard<std::mutex> lk(g_table_mu);
   SharedTable e;
   e.id = g_shared_next++;
   e.device = device;
   e.curve = curve;
-  e.srs = std::move(srs);
+  e.d_key = d_key;
+  e.key_words = key_words;
   e.t = ft;
   e.refs = 1;
   ft.shared = e.id;
@@ -242,6 +283,7 @@ void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, Fi
 void table_share_release(FixedTable& ft) {
   void* d = nullptr;
   uint8_t* inf = nullptr;
+  uint32_t* key = nullptr;
   size_t bytes = 0;
   {
     std::lock_guard<std::mutex> lk(g_table_mu);
@@ -250,6 +292,7 @@ void table_share_release(FixedTable& ft) {
       if (--g_shared[k].refs == 0) {
         d = g_shared[k].t.d;
         inf = g_shared[k].t.inf;
+        key = g_shared[k].d_key;
         bytes = g_shared[k].t.bytes;
         g_shared.erase(g_shared.begin() + (long)k);
       }
@@ -258,23 +301,7 @@ void table_share_release(FixedTable& ft) {
   }
   if (d) table_free(d, bytes);
   if (inf) (void)hipFree(inf);
-}
-
-// a pinned host buffer of at least `words` words for the sharing key's
-// device-to-host copy (per thread, grow-only, kept for the process): a
-// pageable destination sends the copy through the runtime's staging path,
-// which now and then stalls ~16 ms (profiles/r06_kzg_bench_trace_setup.txt)
-uint32_t* pinned_words(size_t words) {
-  thread_local uint32_t* buf = nullptr;
-  thread_local size_t cap = 0;
-  if (words <= cap) return buf;
-  if (buf) (void)hipHostFree(buf);
-  buf = nullptr;
-  cap = 0;
-  const size_t want = std::max<size_t>(words, (size_t)1 << 17);
-  if (hipHostMalloc((void**)&buf, want * 4, hipHostMallocDefault) != hipSuccess) return buf = nullptr;
-  cap = want;
-  return buf;
+  if (key) (void)hipFree(key);
 }
 
 void shared_tables_info(int device, size_t* count, size_t* bytes) {
@@ -486,28 +513,6 @@ int kzgx_init_device(int curve, int device) {
   // the generator comb tables (per process, per device and curve)
   kzgx::GenTables g;
   KZGX_TRY(kzgx::gen_tables_get(curve, device, st, &g));
-  // the default-table sharing key's pinned copy buffer (4097 BLS12-381 points)
-  uint32_t* pw = kzgx::pinned_words((size_t)4097 * 24);
-  if (!pw) return KZGX_ERR_OOM;
-  // every copy path once, each way, pinned and pageable, at sizes past the
-  // runtime's small-copy path: the first copy of a kind in a process pays a
-  // one-time engine setup -- measured 4.7-17 ms on the first 32 KB
-  // device-to-host copy, inside the third setup of the reference benchmark's
-  // sweep (profiles/r06_kzg_bench_trace_setup.txt)
-  {
-    const size_t wb = (size_t)4097 * 24 * 4;
-    void* d = nullptr;
-    KZGX_TRY_HIP(hipMalloc(&d, wb));
-    std::vector<uint8_t> pg(wb, 0);
-    hipError_t e = hipMemcpyAsync(d, pw, wb, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(pw, d, wb, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d, pg.data(), wb, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(pg.data(), d, wb, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync((uint8_t*)d + wb / 2, d, wb / 2, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(d);
-    KZGX_TRY_HIP(e);
-  }
   // the pinned-allocation path of the host-pointer calls
   void* h = nullptr;
   KZGX_TRY_HIP(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
@@ -577,6 +582,7 @@ void kzgx_destroy(kzgx_ctx* ctx) {
     if (w.done) (void)hipEventDestroy(w.done);
   }
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  if (c.small_ev) (void)hipEventDestroy(c.small_ev);
   (void)hipStreamSynchronize(c.stream);
   stream_give(c.device, c.stream);
   kzgx::ctx_live_add(c.device, -1);

@@ -101,11 +101,12 @@ hipError_t table_malloc(void** p, size_t bytes);
 void table_free(void* p, size_t bytes);
 void table_cache_release();
 size_t table_cache_bytes();
-bool table_share_attach(int device, int curve, int c_req, const std::vector<uint32_t>& srs, FixedTable& ft);
-void table_share_register(int device, int curve, std::vector<uint32_t>&& srs, FixedTable& ft);
+bool table_share_attach(int device, int curve, int c_req, const uint32_t* d_canon, size_t key_words, hipStream_t st,
+                        FixedTable& ft);
+void table_share_register(int device, int curve, const uint32_t* d_canon, size_t key_words, hipStream_t st,
+                          FixedTable& ft);
 void table_share_release(FixedTable& ft);
 void shared_tables_info(int device, size_t* count, size_t* bytes);
-uint32_t* pinned_words(size_t words);  // per-thread pinned host scratch (grow-only)
 
 // optional per-kernel timing with HIP events on the launch stream
 struct ProfRec {
@@ -159,6 +160,7 @@ struct Ctx {
   uint32_t* d_table_small = nullptr;
   size_t table_small_bytes = 0;
   size_t n_small = 0;
+  hipEvent_t small_ev = nullptr;  // recorded after the small table's build (small_table_ready)
   // wide-window table of the large single MSMs (msm.hip, msm_big):
   // [W_big][n_srs] at c_big bits, built with an SRS of >= 2^16 points
   uint32_t* d_table_big = nullptr;

@@ -1268,9 +1268,17 @@ int srs_upload_impl(Ctx* ctx, const uint32_t* d_canon, size_t n) {
   // build (the reference benchmark's 128-term setup)
   ctx->n_small = 0;
   // the wide-window table of the large single MSMs (window 0 = the
-  // Montgomery SRS, window 0 of the main table)
+  // Montgomery SRS, window 0 of the main table) -- not when a requested main
+  // fixed-base table will cover every MSM of this SRS (its ~1.3 GB at 2^20
+  // points would only shrink that table's budget), and freed when the SRS
+  // no longer qualifies
   ctx->c_big = 0;
-  if (n >= big_min_points()) {
+  const bool fixed_covers = ctx->fixed.c_req > 0 && ctx->fixed.n_req >= n;
+  if (n < big_min_points() || fixed_covers) {
+    if (ctx->d_table_big) (void)hipFree(ctx->d_table_big);
+    ctx->d_table_big = nullptr;
+    ctx->table_big_bytes = 0;
+  } else {
     const int cb = big_window_bits(n, ctx->curve);
     const int WB = (257 + cb - 1) / cb;
     KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_big, (size_t)WB * n * pw, &ctx->table_big_bytes));
@@ -1396,19 +1404,25 @@ int msm_batch_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, size_t batch, 
 
 // window 0 of the small table is the Montgomery SRS prefix (window 0 of the
 // main table); k_table_build derives the others.  Built on the calling
-// stream and waited for once, so calls on other streams never see it half
-// built.
+// stream and ordered by an event: every later call waits on it on the
+// device, so calls on other streams never see it half built and no _device
+// entry point blocks the host (it was a stream sync).
 template <class C>
 static int small_table_ready(Ctx* ctx, hipStream_t st) {
-  if (ctx->n_small || ctx->c == KZGX_SMALL_WINDOW_BITS || !ctx->n_srs || !ctx->d_table) return KZGX_OK;
+  if (ctx->n_small) {
+    if (ctx->small_ev) KZGX_TRY_HIP(hipStreamWaitEvent(st, ctx->small_ev, 0));
+    return KZGX_OK;
+  }
+  if (ctx->c == KZGX_SMALL_WINDOW_BITS || !ctx->n_srs || !ctx->d_table) return KZGX_OK;
   const size_t pw = affine_words<C>() * sizeof(uint32_t);
   const size_t ns = ctx->n_srs < SMALL_MAX_POINTS ? ctx->n_srs : SMALL_MAX_POINTS;
   constexpr int WS = Win<KZGX_SMALL_WINDOW_BITS>::W;
+  if (!ctx->small_ev) KZGX_TRY_HIP(hipEventCreateWithFlags(&ctx->small_ev, hipEventDisableTiming));
   KZGX_TRY(dev_alloc(ctx, (void**)&ctx->d_table_small, (size_t)WS * ns * pw, &ctx->table_small_bytes));
   KZGX_TRY_HIP(hipMemcpyAsync(ctx->d_table_small, ctx->d_table, ns * pw, hipMemcpyDeviceToDevice, st));
   table_build<C>(ctx->d_table_small, ctx->d_inf, ns, WS, KZGX_SMALL_WINDOW_BITS, st);
   KZGX_TRY_HIP(hipGetLastError());
-  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  KZGX_TRY_HIP(hipEventRecord(ctx->small_ev, st));
   ctx->n_small = ns;
   return KZGX_OK;
 }

@@ -307,21 +307,16 @@ static int fixed_build_default(Ctx* ctx, const uint32_t* d_canon, size_t n_srs) 
   if (ft.c_req == 0 || ft.n_req == 0) return KZGX_OK;
   fixed_free_table(ft);  // its memory counts as free for the choice
   const size_t n = ft.n_req < n_srs ? ft.n_req : n_srs;
-  // the SRS prefix, word for word, is the sharing key (copied through pinned
-  // memory: a pageable destination now and then stalls the copy ~16 ms)
+  // the SRS prefix, word for word, is the sharing key (kept and compared on
+  // the device)
   const size_t kw = (size_t)n * 2 * ctx->base_words();
-  uint32_t* pin = pinned_words(kw);
-  if (!pin) return KZGX_ERR_OOM;
-  KZGX_TRY_HIP(hipMemcpyAsync(pin, d_canon, kw * 4, hipMemcpyDeviceToHost, ctx->stream));
-  KZGX_TRY_HIP(hipStreamSynchronize(ctx->stream));
-  std::vector<uint32_t> key(pin, pin + kw);
-  if (table_share_attach(ctx->device, ctx->curve, ft.c_req, key, ft)) return KZGX_OK;
+  if (table_share_attach(ctx->device, ctx->curve, ft.c_req, d_canon, kw, ctx->stream, ft)) return KZGX_OK;
   auto build = [&](int c) {
     const int keep = ft.c_req;
     ft.c_req = c;
     const int rc = fixed_build_table(ctx, ft, d_canon, n_srs);
     ft.c_req = keep;  // -1: the next SRS picks again
-    if (rc == KZGX_OK && ft.d) table_share_register(ctx->device, ctx->curve, std::move(key), ft);
+    if (rc == KZGX_OK && ft.d) table_share_register(ctx->device, ctx->curve, d_canon, kw, ctx->stream, ft);
     return rc;
   };
   if (ft.c_req > 0) return build(ft.c_req);
