@@ -68,7 +68,9 @@ struct VWave {
   static constexpr int PROD_W = (108 * PL > 32 * 4 * L) ? 108 * PL : 32 * 4 * L;
   static constexpr int O_SCALE = O_PROD + PROD_W;          // [2][3][L] scale factors
   static constexpr int O_FLAG = O_SCALE + 6 * L;           // [16]
-  static constexpr int WORDS = O_FLAG + 16;
+  // the second wave's product parts during the two-wave Miller loop
+  static constexpr int O_PROD2 = (O_FLAG + 16 + 3) & ~3;   // [64][PL]
+  static constexpr int WORDS = O_PROD2 + 64 * PL;
 };
 
 // the wave kernel's LDS (dynamic; V::WORDS words), addressed by word offset
@@ -318,10 +320,13 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   const int lane = threadIdx.x;
-  if (lane < 54) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int t = lane + 54 * h, pr = t / 3;
+  // the 108 parts over the block: two per lane on one wave, one per lane
+  // when the kernel runs two waves (k_verify_wave / k_pair2_wave)
+  const int nt = (int)blockDim.x >= 108 ? 108 : 54;
+  if (lane < nt) {
+#pragma unroll 1
+    for (int t = lane; t < 108; t += nt) {
+      const int pr = t / 3;
       vw_stp<C>(prod + t * PL, vw_part<C>(vw_ld2<C>(a + (pr / 6) * E2), vw_ld2<C>(b + (pr % 6) * E2), t % 3));
     }
   }
@@ -347,13 +352,12 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
 // lane (k, im) < 12 folds the three products landing on w^k (xi for the
 // wrapped ones) lazily
 template <class C>
-KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o) {
+KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o, int lane) {
   using F = typename C::Fp29;
   using V = VWave<C>;
   constexpr int E2 = V::E2, L = V::L, PL = V::PL;
   uint32_t *f = vw_smem + f_o, *prod = vw_smem + prod_o;
   const uint32_t* line = vw_smem + line_o;
-  const int lane = threadIdx.x;
   if (lane < 54) {
     const int i = lane / 9, t = (lane / 3) % 3;
     vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(f + i * E2), vw_ld2<C>(line + t * E2), lane % 3));
@@ -384,12 +388,11 @@ KZGX_DEV int vw_pair_index(int i, int j) {
   return i * 6 - (i * (i - 1)) / 2 + (j - i);
 }
 template <class C>
-KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
+KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o, int lane) {
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t* a = vw_smem + a_o;
-  const int lane = threadIdx.x;
   if (lane < 63) {
     int idx = lane / 3, i = 0;
     while (idx >= 6 - i) {
@@ -511,17 +514,16 @@ template <class C>
 KZGX_DEV void vw_copy(uint32_t dst_o, uint32_t a_o) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
-  for (int w = threadIdx.x; w < VWave<C>::E12; w += 64) dst[w] = a[w];
+  for (int w = threadIdx.x; w < VWave<C>::E12; w += blockDim.x) dst[w] = a[w];
   __syncthreads();
 }
 
 template <class C>
-KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o) {
+KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o, int lane) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
   using F = typename C::Fp29;
   constexpr int L = VWave<C>::L;
-  const int lane = threadIdx.x;
   if (lane < 12) {
     const int k = lane >> 1;
     const F29<F> v = vw_ld<C>(a + lane * L);
@@ -613,7 +615,7 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
   uint32_t* tb = vw_smem + tb_o;
   uint32_t* sc = prod + 64 * L;  // scratch past the parts: F (2L), t (L), F^-1 (2L)
   const int lane = threadIdx.x;
-  vw_conj<C>(ta_o, a_o);
+  vw_conj<C>(ta_o, a_o, lane);
   vw_mul<C>(tb_o, a_o, ta_o, prod_o);
   // (n0, n1, n2) = tb[0], tb[2], tb[4]
   // round A: n0^2, n1 n2, n2^2, n0 n1, n1^2, n0 n2
@@ -741,7 +743,7 @@ KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
     switch (op[0]) {
       case VW_MUL: vw_mul<C>(d, a, b, prod); break;
       case VW_CSQR: vw_cyclo_sqr<C>(d, a, prod); break;
-      case VW_CONJ: vw_conj<C>(d, a); break;
+      case VW_CONJ: vw_conj<C>(d, a, threadIdx.x); break;
       case VW_FROB: vw_frob<C>(d, a, prod); break;
       case VW_INV: vw_inv_wave<C>(d, a, slots + 7 * E, slots + 8 * E, prod); break;
       default: {  // d = a^e (cyclotomic a, top bit of e set), d != a
@@ -761,21 +763,29 @@ KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
           vw_cyclo_sqr<C>(d, d, prod);
           if (((i < 64 ? e0 >> i : e1 >> (i - 64)) & 1ull)) vw_mul<C>(d, d, a, prod);
         }
-        if (op[0] == VW_POWZ && P::Z_NEG) vw_conj<C>(d, d);
+        if (op[0] == VW_POWZ && P::Z_NEG) vw_conj<C>(d, d, threadIdx.x);
       }
     }
   }
 }
 
-// multi-Miller loop of both pairings over the shared loop count, one line
-// product site: line s is a doubling line (square first, except at the top
-// bit), an addition line (after a doubling line of a set bit), or (BN) one of
-// the two Frobenius lines after the conjugation
+// Miller loops of both pairings, one per wave (the kernel runs two waves):
+// wave q squares its own f_q and multiplies in pairing q's lines, so a step
+// costs one squaring and one line product on the critical path instead of a
+// squaring and two line products; then f = f_0 f_1.  Line s is a doubling
+// line (square first, except at the top bit), an addition line (after a
+// doubling line of a set bit), or (BN) one of the two Frobenius lines after
+// the conjugation.  Both waves run the same op sequence, so their barriers
+// pair up; an unused pairing (use_mask bit clear) runs on zeroed lines and
+// its f_q is replaced by 1 before the product.
 template <class C>
 KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
   using P = typename PairOf<C>::T;
   using V = VWave<C>;
   constexpr int NLOOP = V::NL - (P::D_TWIST ? 2 : 0);
+  const int q = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const uint32_t fq = f + (uint32_t)q * V::E12;
+  const uint32_t pq = q ? (uint32_t)V::O_PROD2 : prod;
   int i = P::LOOP_BITS - 2;
   bool add_next = false;
 #pragma unroll 1
@@ -785,18 +795,23 @@ KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
         add_next = false;
         i--;
       } else {
-        if (i != P::LOOP_BITS - 2) vw_sqr<C>(f, f, prod);  // f = 1 before the first line
+        if (i != P::LOOP_BITS - 2) vw_sqr<C>(fq, fq, pq, lane);  // f = 1 before the first line
         add_next = (P::LOOP[i >> 6] >> (i & 63)) & 1ull;
         if (!add_next) i--;
       }
     } else if (s == NLOOP && P::LOOP_NEG) {
-      vw_conj<C>(f, f);
+      vw_conj<C>(fq, fq, lane);
     }
-#pragma unroll 1
-    for (int q = 0; q < 2; q++)
-      if ((use_mask >> q) & 1) vw_mul_line<C>(f, V::O_LINES + (q * V::NL + s) * V::LW, prod);
+    vw_mul_line<C>(fq, V::O_LINES + (q * V::NL + s) * V::LW, pq, lane);
   }
-  if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C>(f, f);
+  if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C>(fq, fq, lane);
+  // f_q = 1 for an unused pairing (uniform per wave), then f = f_0 f_1
+  if (!((use_mask >> q) & 1) && lane < 12) {
+    using F = typename C::Fp29;
+    vw_st<C>(vw_smem + fq + lane * V::L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  }
+  __syncthreads();
+  vw_mul<C>(f, f, f + V::E12, prod);
 }
 
 // The same line table for a variable Q with the G2 chain spread over a wave
@@ -1143,15 +1158,18 @@ KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __rest
   uint32_t* flag = vw_smem + V::O_FLAG;
   const int lane = threadIdx.x;
   const bool use0 = flag[0] != 0, use1 = flag[1] != 0;
-  // ---- scale the precomputed lines
-  for (int t = lane; t < 2 * V::NL * 3; t += 64) {
+  // ---- scale the precomputed lines (zeros for an unused pairing: its
+  // wave's Miller loop then runs on zeros, vw_miller)
+  for (int t = lane; t < 2 * V::NL * 3; t += blockDim.x) {
     const int q = t / (3 * V::NL), c = t % 3;
     const uint32_t* src = vlines + (size_t)t * E2;  // [q][s][c] order matches t
-    vw_st2<C>(lines + t * E2, f2_mul_fp<C>(vw_ld2<C>(src), vw_ld<C>(scale + (q * 3 + c) * L)));
+    const bool use = q ? use1 : use0;
+    vw_st2<C>(lines + t * E2, use ? f2_mul_fp<C>(vw_ld2<C>(src), vw_ld<C>(scale + (q * 3 + c) * L)) : f2_zero<C>());
   }
-  // f = 1
+  // f_0 = f_1 = 1 (slots 0 and 1, one per wave)
   constexpr uint32_t f = V::O_SLOT, pr = V::O_PROD;
-  if (lane < 12) vw_st<C>(vw_smem + f + lane * L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  if ((lane & 63) < 12)
+    vw_st<C>(vw_smem + f + (lane >> 6) * V::E12 + (lane & 63) * L, (lane & 63) == 0 ? f29_one<F>() : f29_zero<F>());
   __syncthreads();
   VW_STAMP(3);
   vw_miller<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr);
@@ -1183,7 +1201,7 @@ KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __rest
 
 // block (one wave) per opening; same contract as k_verify_single
 template <class C>
-__global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__ commits,
+__global__ __launch_bounds__(128) void k_verify_wave(const uint32_t* __restrict__ commits,
                                                     const uint32_t* __restrict__ commit_inf,
                                                     const uint32_t* __restrict__ proofs,
                                                     const uint32_t* __restrict__ proof_inf,
@@ -1258,7 +1276,7 @@ __global__ __launch_bounds__(64) void k_verify_wave(const uint32_t* __restrict__
 // of verify_proof with more than one point (e(pi, [Z(tau)]G2) ==
 // e(C - [I(tau)]G1, G2[0]))
 template <class C>
-__global__ __launch_bounds__(64) void k_pair2_wave(const uint32_t* __restrict__ p, const uint32_t* __restrict__ p_inf,
+__global__ __launch_bounds__(128) void k_pair2_wave(const uint32_t* __restrict__ p, const uint32_t* __restrict__ p_inf,
                                                    const uint32_t* __restrict__ q_inf,
                                                    const uint32_t* __restrict__ vlines,
                                                    const uint32_t* __restrict__ qfin, uint32_t* __restrict__ ok) {
@@ -1304,8 +1322,8 @@ __global__ __launch_bounds__(64) void k_vw_bench(int op, uint32_t iters, uint64_
     switch (op) {
       case 0: vw_cyclo_sqr<C>(s0, s0, V::O_PROD); break;
       case 1: vw_mul<C>(s0, s0, s1, V::O_PROD); break;
-      case 2: vw_sqr<C>(s0, s0, V::O_PROD); break;
-      case 3: vw_mul_line<C>(s0, V::O_LINES, V::O_PROD); break;
+      case 2: vw_sqr<C>(s0, s0, V::O_PROD, lane); break;
+      case 3: vw_mul_line<C>(s0, V::O_LINES, V::O_PROD, lane); break;
       case 4: vw_frob<C>(s0, s0, V::O_PROD); break;
       case 5: vw_inv<C>(s1, s0); break;
       default: vw_inv_wave<C>(s1, s0, s1 + V::E12, s1 + 2 * V::E12, V::O_PROD); break;
@@ -1383,7 +1401,7 @@ static int verify_wave_impl(const uint32_t* d_commits, const uint32_t* d_commit_
                             const uint32_t* d_g1_0, const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st) {
   const uint32_t* lines = d_buf + vw_tab_words<C>();
   const uint32_t* qfin = lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
-  hipLaunchKernelGGL(k_verify_wave<C>, dim3((unsigned)count), dim3(64), VWave<C>::WORDS * 4, st, d_commits, d_commit_inf, d_proofs,
+  hipLaunchKernelGGL(k_verify_wave<C>, dim3((unsigned)count), dim3(128), VWave<C>::WORDS * 4, st, d_commits, d_commit_inf, d_proofs,
                      d_proof_inf, d_z, d_y, (uint32_t)count, d_g1_0, d_buf, lines, qfin, d_ok);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
@@ -1407,7 +1425,7 @@ static int pair2_wave_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const u
   uint32_t* qfin = d_lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
   hipLaunchKernelGGL(k_vlines_wave<C>, dim3(2), dim3(64), VLine<C>::WORDS * 4, st, d_q, d_lines, qfin, qfin + 2);
   hipLaunchKernelGGL(k_vlines_redo<C>, dim3(1), dim3(64), 0, st, d_q, d_lines, qfin + 2);
-  hipLaunchKernelGGL(k_pair2_wave<C>, dim3(1), dim3(64), VWave<C>::WORDS * 4, st, d_p, d_p_inf, d_q_inf, d_lines,
+  hipLaunchKernelGGL(k_pair2_wave<C>, dim3(1), dim3(128), VWave<C>::WORDS * 4, st, d_p, d_p_inf, d_q_inf, d_lines,
                      qfin, d_ok);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
