@@ -74,7 +74,8 @@ def parse():
     ap.add_argument("--fixed-bits", type=int, default=-1,
                     help="fixed-base table window (0 = Pippenger only; default BN254 17: 15 windows, "
                          "257.8 GB of 64-B entries; BLS12-381 16: 240.6 GB of 112-B entries, of the 288 GiB HBM; "
-                         "a window that does not fit steps down; cfg5 default 0: the wide-window Pippenger)")
+                         "a window that does not fit steps down; cfg5 default: a c <= 10 table over shards of <= 2^18 + 1 "
+                         "points, else 0: the wide-window Pippenger)")
     ap.add_argument("--fixed-ppt", type=int, default=-1,
                     help="SRS points per accumulation thread (fixed-base path; 0 = automatic; default cfg2 22: "
                          "2048 MSMs x 3 wavefronts = two full residencies per launch; cfg4 65: 2048 x 1 wavefront; "
@@ -960,8 +961,14 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     # whose table fits the free HBM (2^20 points on 1 GPU: c = 8, 274.9 GB;
     # 2^19 on 2: c = 9; 2^18 on 4: c = 10; 2^17 on 8: c = 11), point-major
     # (msm_fixed.hip).  Setup work, outside the timed region.
+    # Round 6, automatic choice (no --fixed-bits): a shard of <= 2^18 + 1
+    # points (4 ranks and more) gets the fixed-base table over its points at
+    # the widest window <= 10 that fits (131 073 points: c = 10, 111.7 GB,
+    # 0.44 ms per partial against 0.68 ms on the wide-window path,
+    # profiles/r06_shard_fixed.jsonl); larger shards stay table-free (2^20 + 1
+    # points: c = 8 would run 3.05 ms against 2.05 ms).
     t_setup = time.perf_counter()
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else 0
+    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (10 if count <= (1 << 18) + 1 else 0)
     if fixed_bits:
         fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1),
                                              budget=args.table_gb * 1e9 if args.table_gb > 0 else None)

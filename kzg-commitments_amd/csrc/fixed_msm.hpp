@@ -338,14 +338,18 @@ KZGX_DEV void lat_store_affine(const Xyzz<C>& acc, uint32_t b, uint32_t lane, ui
 // consecutive terms [t Q, t Q + Q): every thread does Q or fewer additions.
 // A thread that starts inside point i runs the digit recoding of i's lower
 // windows for their carry only.  The lookup of the next term is in flight
-// during the addition of the current one, and the wavefront folds its 64
-// partials with 6 shuffle additions before one lane stores (the first 64:1
-// level of the reduction, without a launch).
+// during the addition of the current one.  lane_parts: every thread stores
+// its partial (part[b][t], for k_fixed_fold3); else the wavefront folds its
+// 64 partials with 6 shuffle additions before one lane stores (round 5: the
+// first 64:1 level of the reduction without a launch -- but 6 full additions
+// on every one of the ~3 resident waves per SIMD, ~90 us of a 131 073-point
+// shard's 0.4 ms accumulation).
 // --------------------------------------------------------------------------
 template <class C, int CB>
 __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat(
     const uint32_t* __restrict__ scalars, uint32_t n, size_t stride_words, const uint32_t* __restrict__ tab,
-    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t Q, uint32_t T, uint32_t* __restrict__ part) {
+    TabStrides ts, const uint8_t* __restrict__ inf, uint32_t Q, uint32_t T, uint32_t* __restrict__ part,
+    uint32_t lane_parts) {
   constexpr int PW = packed_words<C>();
   constexpr int XW = xyzz_words<C>();
   constexpr int W = FixedWin<C, CB>::W;
@@ -418,9 +422,65 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
       }
     }
   }
+  if (lane_parts) {
+    xyzz_store<C>(part + ((size_t)b * T + t) * XW, acc);
+    return;
+  }
 #pragma unroll 1
   for (int off = 32; off >= 1; off >>= 1) acc = xyzz_shfl_xor_add<C>(acc, off);
   if (threadIdx.x == 0) xyzz_store<C>(part + ((size_t)b * (T / 64) + t / 64) * XW, acc);
+}
+
+// The flat path's reduction in one launch (three fold levels, arrival
+// counters as k_fixed_accum_lat): wavefront q < P1 of MSM b folds partials
+// [q per, q per + per) (lat_fold: strided sums, then the butterfly with
+// cooperative last levels) into part2[b][q]; the last wavefront of each
+// group of 64 to arrive folds its group's sums into part3[b][grp]; the last
+// of the NG group folders folds those into the result -- the XYZZ record
+// (xyzz_out) or the canonical affine point.  Three levels of <= 64 partials
+// on mostly idle SIMDs, each a few dependent additions, instead of a 6-level
+// shuffle fold in every accumulating wavefront plus two reduce launches
+// (131 073-point shard at c = 10: 0.22 ms of reduction in round 5).
+// cnt[b (NG + 1)]: the final counter, then one per group; each is zeroed by
+// the wavefront that consumes it (stream order makes the next call see 0).
+template <class C>
+__global__ __launch_bounds__(64) void k_fixed_fold3(const uint32_t* __restrict__ part, uint32_t per, uint32_t P1,
+                                                    uint32_t NG, uint32_t* __restrict__ part2,
+                                                    uint32_t* __restrict__ part3, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ out_inf,
+                                                    uint32_t* __restrict__ xyzz_out) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t b = blockIdx.y, q = blockIdx.x, lane = threadIdx.x;
+  Xyzz<C> s = lat_fold<C>(part + ((size_t)b * P1 * per + (size_t)q * per) * XW, per, lane, true);
+  uint32_t* cb = cnt + (size_t)b * (NG + 1);
+  const uint32_t grp = q >> 6;
+  uint32_t prev = 0;
+  if (lane == 0) {
+    xyzz_store<C>(part2 + ((size_t)b * P1 + q) * XW, s);
+    __threadfence();
+    prev = atomicAdd(cb + 1 + grp, 1u);
+  }
+  prev = __shfl(prev, 0, 64);
+  const uint32_t gsz = P1 - grp * 64 < 64 ? P1 - grp * 64 : 64;
+  if (prev + 1 != gsz) return;
+  __threadfence();
+  s = lat_fold<C>(part2 + ((size_t)b * P1 + grp * 64) * XW, gsz, lane, true);
+  if (lane == 0) {
+    cb[1 + grp] = 0;  // every arrival of the group is in
+    xyzz_store<C>(part3 + ((size_t)b * NG + grp) * XW, s);
+    __threadfence();
+    prev = atomicAdd(cb, 1u);
+  }
+  prev = __shfl(prev, 0, 64);
+  if (prev + 1 != NG) return;
+  __threadfence();
+  s = lat_fold<C>(part3 + (size_t)b * NG * XW, NG, lane, true);
+  if (lane == 0) cb[0] = 0;
+  if (xyzz_out) {
+    if (lane == 0) xyzz_store<C>(xyzz_out + (size_t)b * XW, s);
+    return;
+  }
+  lat_store_affine<C>(s, b, lane, out, out_inf);
 }
 
 template <class C, int CB>
@@ -493,12 +553,39 @@ int fixed_msm_win(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n,
       WsLease wsp = ctx->ws_for(st);
       if (!wsp) return KZGX_ERR_ARG;
       MsmWs& ws = *wsp;
+      // round 6: per-lane partials and the one-launch three-level fold
+      // (k_fixed_fold3); KZGX_FLAT_WAVEFOLD=1 keeps round 5's in-wave fold
+      // and reduce launches (A/B)
+      static const bool wavefold = std::getenv("KZGX_FLAT_WAVEFOLD") && std::getenv("KZGX_FLAT_WAVEFOLD")[0] == '1';
+      constexpr size_t kCnt = 16 * 17;  // the lat path's counter block
+      // per: partials per first-level wavefront (KZGX_FOLD3_PER, A/B: 64 / 128 / 256)
+      static const uint32_t per = std::getenv("KZGX_FOLD3_PER") ? (uint32_t)std::strtoul(std::getenv("KZGX_FOLD3_PER"), nullptr, 10) : 256u;
+      const uint32_t P1 = T / per, NG = (P1 + 63) / 64;  // T is a multiple of 4096
+      if (!wavefold && (per == 64 || per == 128 || per == 256) && batch * (NG + 1) <= kCnt) {
+        KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * (size_t)T * XB, &ws.fpart_b));
+        KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * (size_t)(P1 + NG) * XB, &ws.fsum_b));
+        if (!ws.lat_cnt) {  // arrival counters, zero between calls
+          KZGX_TRY_HIP(hipMalloc((void**)&ws.lat_cnt, kCnt * sizeof(uint32_t)));
+          KZGX_TRY_HIP(hipMemsetAsync(ws.lat_cnt, 0, kCnt * sizeof(uint32_t), st));
+        }
+        {
+          ProfScope p(ctx, st, "msm_accum");
+          hipLaunchKernelGGL((k_fixed_accum_flat<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
+                             (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), Q, T, ws.fpart, 1u);
+        }
+        ProfScope p(ctx, st, "msm_reduce");
+        hipLaunchKernelGGL(k_fixed_fold3<C>, dim3(P1, (unsigned)batch), dim3(64), 0, st, ws.fpart, per, P1, NG,
+                           ws.fsum, ws.fsum + batch * (size_t)P1 * xyzz_words<C>(), ws.lat_cnt, d_out, d_out_inf,
+                           xyzz_out);
+        KZGX_TRY_HIP(hipGetLastError());
+        return KZGX_OK;
+      }
       KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * (T / 64) * XB, &ws.fpart_b));
       KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * (T / 4096) * XB, &ws.fsum_b));
       {
         ProfScope p(ctx, st, "msm_accum");
         hipLaunchKernelGGL((k_fixed_accum_flat<C, CB>), dim3(T / 64, (unsigned)batch), dim3(64), 0, st, d_scalars,
-                           (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), Q, T, ws.fpart);
+                           (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), Q, T, ws.fpart, 0u);
       }
       ProfScope p(ctx, st, "msm_reduce");
       // T / 64 wavefront partials per MSM: one more 64:1 level, then one

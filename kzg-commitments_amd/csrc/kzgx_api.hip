@@ -1471,6 +1471,33 @@ int kzgx_verify_single_batch(kzgx_ctx* ctx, const uint64_t* commits_xy, const in
   if (count == 0) return KZGX_OK;
   if (!commits_xy || !proofs_xy || !zs || !ys || !ok || count > (1u << 26)) return KZGX_ERR_ARG;
   const size_t pb = point_words(ctx) * 4;
+  if (count <= ctx->vw_max && count * (2 * pb + 76) <= PIN_DIRECT_MAX) {
+    // the wave path (single verify_proof calls): inputs and the result in
+    // the context's mapped pinned staging -- the kernel copies each opening's
+    // inputs into LDS in one round trip and writes its boolean straight into
+    // host memory, so the call makes no copy at all (it made five H2D and
+    // one D2H copies from pageable memory, ~10 us each)
+    const size_t o_ok = 0, o_c = align256(count * 4), o_p = o_c + align256(count * pb);
+    const size_t o_z = o_p + align256(count * pb), o_y = o_z + count * 32, o_f = align256(o_y + count * 32);
+    KZGX_TRY(pin_stage(ctx, o_f + count * 8));
+    uint8_t* h = ctx->h_pin;
+    std::memcpy(h + o_c, commits_xy, count * pb);
+    std::memcpy(h + o_p, proofs_xy, count * pb);
+    std::memcpy(h + o_z, zs, count * 32);
+    std::memcpy(h + o_y, ys, count * 32);
+    uint32_t* hf = reinterpret_cast<uint32_t*>(h + o_f);
+    for (size_t k = 0; k < count; k++) {
+      hf[k] = commit_inf ? (uint32_t)(commit_inf[k] != 0) : 0u;
+      hf[count + k] = proof_inf ? (uint32_t)(proof_inf[k] != 0) : 0u;
+    }
+    uint8_t* d = ctx->d_pin;
+    KZGX_TRY(kzgx_verify_single_batch_device(ctx, d + o_c, d + o_f, d + o_p, d + o_f + count * 4, d + o_z, d + o_y,
+                                             count, d + o_ok, nullptr));
+    KZGX_TRY_HIP(hipStreamSynchronize(ctx->c.stream));
+    const uint32_t* v = reinterpret_cast<const uint32_t*>(h + o_ok);
+    for (size_t k = 0; k < count; k++) ok[k] = (int)v[k];
+    return KZGX_OK;
+  }
   void *d_c, *d_p, *d_s, *d_f;
   KZGX_TRY(stage(ctx, 0, count * pb, &d_c));
   KZGX_TRY(stage(ctx, 1, count * pb, &d_p));

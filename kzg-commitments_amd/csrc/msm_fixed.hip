@@ -171,7 +171,15 @@ __global__ __launch_bounds__(64) void k_fixed_finish(const uint32_t* __restrict_
 
 template <class C>
 void fixed_reduce_launch(const uint32_t* part, uint32_t T, uint32_t batch, uint32_t* sums, hipStream_t st) {
-  hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((batch + 3) / 4), dim3(256), 0, st, part, T, batch, sums);
+  // one wavefront per workgroup: a 131 073-point shard's 64:1 level over 48
+  // wavefronts took 77 us against 116 us as 4-wave workgroups (r06
+  // profiles; the waves of a workgroup do land on 4 different SIMDs,
+  // scripts/probe_simd.hip).  KZGX_REDUCE_WG256=1: the round-5 launch (A/B)
+  static const bool wg256 = std::getenv("KZGX_REDUCE_WG256") != nullptr;
+  if (!wg256)
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3(batch), dim3(64), 0, st, part, T, batch, sums);
+  else
+    hipLaunchKernelGGL(k_fixed_reduce<C>, dim3((batch + 3) / 4), dim3(256), 0, st, part, T, batch, sums);
 }
 template <class C>
 void fixed_finish_launch(const uint32_t* sums, uint32_t batch, uint32_t* out, uint32_t* out_inf, uint32_t* xyzz_out,

@@ -70,7 +70,13 @@ struct VWave {
   static constexpr int O_FLAG = O_SCALE + 6 * L;           // [16]
   // the second wave's product parts during the two-wave Miller loop
   static constexpr int O_PROD2 = (O_FLAG + 16 + 3) & ~3;   // [64][PL]
-  static constexpr int WORDS = O_PROD2 + 64 * PL;
+  // one opening's inputs, copied in at the kernel's start (the host entry
+  // point passes them in mapped pinned memory: one PCIe round trip, not one
+  // per access): commit (2N) | proof (2N) | z (8) | y (8) | commit_inf | proof_inf
+  static constexpr int NW = C::Fp::N;
+  static constexpr int I_C = 0, I_P = 2 * NW, I_Z = 4 * NW, I_Y = 4 * NW + 8, I_CINF = 4 * NW + 16, I_PINF = I_CINF + 1;
+  static constexpr int O_IN = O_PROD2 + 64 * PL;
+  static constexpr int WORDS = O_IN + I_PINF + 1;
 };
 
 // the wave kernel's LDS (dynamic; V::WORDS words), addressed by word offset
@@ -1172,6 +1178,10 @@ KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __rest
     vw_st<C>(vw_smem + f + (lane >> 6) * V::E12 + (lane & 63) * L, (lane & 63) == 0 ? f29_one<F>() : f29_zero<F>());
   __syncthreads();
   VW_STAMP(3);
+#ifdef KZGX_VW_TIMING
+  // which SIMD each of the two waves runs on (HW_ID bits 5:4; CU 11:8)
+  if ((threadIdx.x & 63) == 0) vw_ts[10 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
   vw_miller<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr);
   VW_STAMP(4);
   vw_final_exp<C>(V::O_SLOT, pr);
@@ -1195,6 +1205,9 @@ KZGX_DEV void vw_pair_tail(const uint32_t* __restrict__ vlines, uint32_t* __rest
              (unsigned long long)(vw_ts[1] - vw_ts[0]), (unsigned long long)(vw_ts[2] - vw_ts[1]),
              (unsigned long long)(vw_ts[3] - vw_ts[2]), (unsigned long long)(vw_ts[4] - vw_ts[3]),
              (unsigned long long)(vw_ts[8] - vw_ts[4]));
+    if (blockIdx.x == 0)
+      printf("vw_hwid wave0 simd %u cu %u  wave1 simd %u cu %u\n", (unsigned)((vw_ts[10] >> 4) & 3),
+             (unsigned)((vw_ts[10] >> 8) & 15), (unsigned)((vw_ts[11] >> 4) & 3), (unsigned)((vw_ts[11] >> 8) & 15));
 #endif
   }
 }
@@ -1219,11 +1232,22 @@ __global__ __launch_bounds__(128) void k_verify_wave(const uint32_t* __restrict_
   const int lane = threadIdx.x;
   if (k >= count) return;  // uniform over the block
   VW_STAMP(0);
+  // the opening's inputs into LDS, one word per thread (inputs may live in
+  // mapped host memory: every later read is then an LDS read)
+  uint32_t* in = vw_smem + V::O_IN;
+  static_assert(V::I_PINF < 128, "k_verify_wave: one input word per thread");
+  if (lane < V::I_P) in[lane] = commits[(size_t)k * 2 * N + lane];
+  else if (lane < V::I_Z) in[lane] = proofs[(size_t)k * 2 * N + lane - V::I_P];
+  else if (lane < V::I_Y) in[lane] = zs[(size_t)k * 8 + lane - V::I_Z];
+  else if (lane < V::I_CINF) in[lane] = ys[(size_t)k * 8 + lane - V::I_Y];
+  else if (lane == V::I_CINF) in[lane] = commit_inf ? commit_inf[k] : 0u;
+  else if (lane == V::I_PINF) in[lane] = proof_inf ? proof_inf[k] : 0u;
+  __syncthreads();
   // ---- [y]G: lane w takes window w's table entry, then a 5-level tree
   Affine<C> g;
   const bool gf = affine_from_canonical<C>(g1_0, g);
   if (lane < 32) {
-    const uint32_t d = (ys[(size_t)k * 8 + (lane >> 2)] >> (8 * (lane & 3))) & 255u;
+    const uint32_t d = (in[V::I_Y + (lane >> 2)] >> (8 * (lane & 3))) & 255u;
     Xyzz<C> p = xyzz_inf<C>();
     if (gf && d) p = xyzz_from_affine<C>(affine_load<C>(vtab + ((size_t)lane * 255 + d - 1) * V::AW));
     xyzz_store<C>(prod + lane * 4 * L, p);
@@ -1239,18 +1263,18 @@ __global__ __launch_bounds__(128) void k_verify_wave(const uint32_t* __restrict_
   // ---- D = C - [y]G + [z]pi and the per-pairing scale factors (lane 0)
   if (lane == 0) {
     Affine<C> c, pi;
-    const bool cf = affine_from_canonical<C>(commits + (size_t)k * 2 * N, c) && !(commit_inf && commit_inf[k]);
-    const bool pf = affine_from_canonical<C>(proofs + (size_t)k * 2 * N, pi) && !(proof_inf && proof_inf[k]);
+    const bool cf = affine_from_canonical<C>(in + V::I_C, c) && !in[V::I_CINF];
+    const bool pf = affine_from_canonical<C>(in + V::I_P, pi) && !in[V::I_PINF];
     Xyzz<C> d = xyzz_neg<C>(xyzz_load<C>(prod));
     if (cf) d = xyzz_add_affine<C>(d, c);
     if (pf) {
       int top = -1;
       for (int b = 255; b >= 0 && top < 0; b--)
-        if ((zs[(size_t)k * 8 + (b >> 5)] >> (b & 31)) & 1u) top = b;
+        if ((in[V::I_Z + (b >> 5)] >> (b & 31)) & 1u) top = b;
       Xyzz<C> zp = xyzz_inf<C>();
       for (int b = top; b >= 0; b--) {
         zp = xyzz_dbl<C>(zp);
-        if ((zs[(size_t)k * 8 + (b >> 5)] >> (b & 31)) & 1u) zp = xyzz_add_affine<C>(zp, pi);
+        if ((in[V::I_Z + (b >> 5)] >> (b & 31)) & 1u) zp = xyzz_add_affine<C>(zp, pi);
       }
       d = xyzz_add<C>(d, zp);
     }
