@@ -451,7 +451,18 @@ __global__ __launch_bounds__(64) void k_fixed_fold3(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ xyzz_out) {
   constexpr int XW = xyzz_words<C>();
   const uint32_t b = blockIdx.y, q = blockIdx.x, lane = threadIdx.x;
-  Xyzz<C> s = lat_fold<C>(part + ((size_t)b * P1 * per + (size_t)q * per) * XW, per, lane, true);
+  const uint32_t* src = part + ((size_t)b * P1 * per + (size_t)q * per) * XW;
+  Xyzz<C> s;
+  if (per == 256 || per == 512) {
+    // the lane's 4 (8) strided partials as a tree of independent additions
+    // (depth 2 (3)) instead of a chain of 3 (7)
+    auto ld = [&](int k) { return xyzz_load<C>(src + (size_t)(lane + 64 * k) * XW); };
+    s = xyzz_add_impl<C>(xyzz_add_impl<C>(ld(0), ld(1)), xyzz_add_impl<C>(ld(2), ld(3)));
+    if (per == 512) s = xyzz_add_impl<C>(s, xyzz_add_impl<C>(xyzz_add_impl<C>(ld(4), ld(5)), xyzz_add_impl<C>(ld(6), ld(7))));
+    s = xyzz_wave_sum<C>(s, lane, true);
+  } else {
+    s = lat_fold<C>(src, per, lane, true);
+  }
   uint32_t* cb = cnt + (size_t)b * (NG + 1);
   const uint32_t grp = q >> 6;
   uint32_t prev = 0;
@@ -561,7 +572,7 @@ int fixed_msm_win(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n,
       // per: partials per first-level wavefront (KZGX_FOLD3_PER, A/B: 64 / 128 / 256)
       static const uint32_t per = std::getenv("KZGX_FOLD3_PER") ? (uint32_t)std::strtoul(std::getenv("KZGX_FOLD3_PER"), nullptr, 10) : 256u;
       const uint32_t P1 = T / per, NG = (P1 + 63) / 64;  // T is a multiple of 4096
-      if (!wavefold && (per == 64 || per == 128 || per == 256) && batch * (NG + 1) <= kCnt) {
+      if (!wavefold && (per == 64 || per == 128 || per == 256 || per == 512) && batch * (NG + 1) <= kCnt) {
         KZGX_TRY(dev_alloc(ctx, (void**)&ws.fpart, batch * (size_t)T * XB, &ws.fpart_b));
         KZGX_TRY(dev_alloc(ctx, (void**)&ws.fsum, batch * (size_t)(P1 + NG) * XB, &ws.fsum_b));
         if (!ws.lat_cnt) {  // arrival counters, zero between calls
