@@ -12,6 +12,7 @@
 #ifndef KZGX_VW_CHAIN
 #define KZGX_FIELD_LATENCY
 #endif
+#include "coop.hpp"
 #include "pairing_common.hpp"
 #include "kzgx_setup.hpp"
 
@@ -57,7 +58,7 @@ struct VWave {
   static constexpr int AW = affine_words<C>();
   // positions of the w0, w1, w3 coefficients in the w basis
   static constexpr int POS0 = P::D_TWIST ? 0 : 3, POS1 = P::D_TWIST ? 1 : 2, POS3 = P::D_TWIST ? 3 : 0;
-  static constexpr int NSLOT = 9;
+  static constexpr int NSLOT = 15;  // 0..8: the final exponentiation's program, 9..14: the second wave's
   // LDS carve (words)
   static constexpr int O_LINES = 0;                        // [2][NL][LW] scaled lines
   static constexpr int O_SLOT = O_LINES + 2 * NL * LW;     // [NSLOT][E12]
@@ -69,13 +70,13 @@ struct VWave {
   static constexpr int O_SCALE = O_PROD + PROD_W;          // [2][3][L] scale factors
   static constexpr int O_FLAG = O_SCALE + 6 * L;           // [16]
   // the second wave's product parts during the two-wave Miller loop
-  static constexpr int O_PROD2 = (O_FLAG + 16 + 3) & ~3;   // [64][PL]
+  static constexpr int O_PROD2 = (O_FLAG + 16 + 3) & ~3;   // [108][PL]
   // one opening's inputs, copied in at the kernel's start (the host entry
   // point passes them in mapped pinned memory: one PCIe round trip, not one
   // per access): commit (2N) | proof (2N) | z (8) | y (8) | commit_inf | proof_inf
   static constexpr int NW = C::Fp::N;
   static constexpr int I_C = 0, I_P = 2 * NW, I_Z = 4 * NW, I_Y = 4 * NW + 8, I_CINF = 4 * NW + 16, I_PINF = I_CINF + 1;
-  static constexpr int O_IN = O_PROD2 + 64 * PL;
+  static constexpr int O_IN = O_PROD2 + 108 * PL;
   static constexpr int WORDS = O_IN + I_PINF + 1;
 };
 
@@ -314,21 +315,36 @@ KZGX_DEV void lin_add_f2p(LinAcc<F>& acc, const uint32_t* q, int im, bool xi, in
   lin_addp<F>(acc, q + 2 * PL, d * c2);
 }
 
+// The ops' synchronisation: a workgroup barrier (WS = false: every wave of
+// the block runs the same op sequence), or (WS = true: each wave runs its own
+// sequence on its own slots and product parts, vw_hard_bn2) only this wave's
+// LDS accesses completed and a compiler barrier -- a wave's lanes exchange
+// through LDS with no other wave involved
+template <bool WS>
+KZGX_DEV void vw_sync() {
+  if constexpr (WS) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  else __syncthreads();
+}
+template <bool WS>
+KZGX_DEV int vw_lane() {
+  return WS ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+}
+
 // ---- Fp12 (w basis) in LDS, wave-cooperative; every op ends with a barrier
 // dst = a b (dst may alias a or b): the 36 Fp2 products a_i b_j as 108 Fp
 // (Karatsuba) parts, two independent products per lane (54 lanes), then lane
 // (k, im) < 12 folds the six products landing on w^k (xi for the wrapped
 // ones) lazily
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o) {
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t *a = vw_smem + a_o, *b = vw_smem + b_o;
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   // the 108 parts over the block: two per lane on one wave, one per lane
-  // when the kernel runs two waves (k_verify_wave / k_pair2_wave)
-  const int nt = (int)blockDim.x >= 108 ? 108 : 54;
+  // when the kernel runs two waves (k_verify_wave / k_pair2_wave) in step
+  const int nt = (!WS && (int)blockDim.x >= 108) ? 108 : 54;
   if (lane < nt) {
 #pragma unroll 1
     for (int t = lane; t < 108; t += nt) {
@@ -336,7 +352,7 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
       vw_stp<C>(prod + t * PL, vw_part<C>(vw_ld2<C>(a + (pr / 6) * E2), vw_ld2<C>(b + (pr % 6) * E2), t % 3));
     }
   }
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 12) {
     // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij
     const int k = lane >> 1, im = lane & 1;
@@ -350,7 +366,7 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
     }
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // f = f l for a scaled line l = (l0, l1, l3) at positions (POS0, POS1, POS3):
@@ -455,13 +471,13 @@ KZGX_DEV F29<F> vw_norm(const uint32_t (&o)[F::L]) {
   }
   return r;
 }
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t* a = vw_smem + a_o;
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   if (lane < 18) {
     const int j = lane / 6, which = (lane / 3) & 1, part = lane % 3;
     const uint32_t *xp = a + j * E2, *yp = a + (j + 3) * E2;
@@ -480,7 +496,7 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     }
     vw_stp<C>(prod + lane * PL, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
   }
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 12) {
     const int k = lane >> 1, im = lane & 1;
     const int j = (k & 1) ? (k == 3 ? 0 : k == 5 ? 1 : 2) : (k >> 1);
@@ -513,18 +529,18 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     lin_add<F>(acc, a + k * E2 + im * L, (k & 1) ? 2 : -2);
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_copy(uint32_t dst_o, uint32_t a_o) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
-  for (int w = threadIdx.x; w < VWave<C>::E12; w += blockDim.x) dst[w] = a[w];
-  __syncthreads();
+  for (int w = vw_lane<WS>(); w < VWave<C>::E12; w += WS ? 64 : (int)blockDim.x) dst[w] = a[w];
+  vw_sync<WS>();
 }
 
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o, int lane) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
@@ -535,13 +551,13 @@ KZGX_DEV void vw_conj(uint32_t dst_o, uint32_t a_o, int lane) {
     const F29<F> v = vw_ld<C>(a + lane * L);
     vw_st<C>(dst + lane * L, (k & 1) ? fp_neg<F>(v) : v);
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // dst = a^p: coefficient k is conj(a_k) g_k (g_k = P::FROB[k]); lane (k, t)
 // < 24 forms one of the four Fp products of conj(a_k) g_k, lane (k, im) < 12
 // folds re = a.re g.re + a.im g.im, im = a.re g.im - a.im g.re
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
@@ -549,7 +565,7 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using P = typename PairOf<C>::T;
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   if (lane < 24) {
     const int k = lane >> 2, t = lane & 3;
     // t: 0 a.re g.re, 1 a.im g.im, 2 a.re g.im, 3 a.im g.re
@@ -565,7 +581,7 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     // Frobenius against the latency-first form (profiles/r05_vw_ops_ab.json)
     vw_stp<C>(prod + lane * PL, f29_mul_chain<F>(vw_ld<C>(a + k * E2 + ((t & 1) ? L : 0)), g));
   }
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 12) {
     const int k = lane >> 1, im = lane & 1;
     const uint32_t* q = prod + k * 4 * PL;
@@ -575,7 +591,7 @@ KZGX_DEV void vw_frob(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     lin_addp<F>(acc, q + (im ? 3 : 1) * PL, im ? -1 : 1);
     vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // one lane: the tower inverse
@@ -711,26 +727,39 @@ KZGX_TW void vw_inv_wave(uint32_t dst_o, uint32_t a_o, uint32_t ta_o, uint32_t t
 // final exponentiation as a small program over Fp12 slots (the chains of
 // final_exp), run by one loop so that every wave-wide op is inlined once and
 // no call (with its register save / restore through scratch) sits between
-// rounds.  Slots: 0 f, 1 g, 2 t0, 3 t1, 4 a, 5 b, 6 c, 7 t2, 8 t3.
-enum : uint8_t { VW_MUL, VW_CSQR, VW_CONJ, VW_FROB, VW_INV, VW_POWZ, VW_POWS, VW_POWK3 };
-// easy part f^(p^6 - 1)(p^2 + 1) -> g, then the BN254 hard part in u, with
-// a = g^u, b = a^u, c = b^u:  f = conj(c^36 b^30 a^18 g^2)
-// (conj(c^36 b^18 a^12) g)^p (b^6 g)^(p^2) g^(p^3).  The small powers share
-// one chain per base (b^2, b^3, b^6, b^12, b^18 = b^12 b^6, b^30 = b^18 b^12;
-// a^3, a^6, a^12, a^18): 11 cyclotomic squarings + 6 products instead of
-// 22 + 8 as separate powers (round 4 form).
-__constant__ uint8_t vw_fe_bn[][4] = {
-    {VW_INV, 2, 0, 0},   {VW_CONJ, 1, 0, 0},  {VW_MUL, 1, 1, 2},   {VW_FROB, 2, 1, 0},  {VW_FROB, 2, 2, 0},
-    {VW_MUL, 1, 2, 1},   {VW_POWZ, 4, 1, 0},  {VW_POWZ, 5, 4, 0},  {VW_POWZ, 6, 5, 0},  {VW_POWS, 2, 6, 36},
-    // b^6 -> 6, b^12 -> 7, b^18 -> 8, b^30 -> 3
-    {VW_CSQR, 6, 5, 0},  {VW_MUL, 6, 6, 5},   {VW_CSQR, 6, 6, 0},  {VW_CSQR, 7, 6, 0},  {VW_MUL, 8, 7, 6},
-    {VW_MUL, 3, 8, 7},   {VW_MUL, 0, 2, 3},
-    // a^6 -> 5, a^12 -> 7, a^18 -> 3
-    {VW_CSQR, 5, 4, 0},  {VW_MUL, 5, 5, 4},   {VW_CSQR, 5, 5, 0},  {VW_CSQR, 7, 5, 0},  {VW_MUL, 3, 7, 5},
-    {VW_MUL, 0, 0, 3},   {VW_CSQR, 3, 1, 0},  {VW_MUL, 0, 0, 3},   {VW_CONJ, 0, 0, 0},
-    {VW_MUL, 3, 8, 7},   {VW_MUL, 3, 2, 3},   {VW_CONJ, 3, 3, 0},  {VW_MUL, 3, 3, 1},   {VW_MUL, 7, 6, 1},
-    {VW_FROB, 3, 3, 0},  {VW_MUL, 0, 0, 3},   {VW_FROB, 7, 7, 0},  {VW_FROB, 7, 7, 0},  {VW_MUL, 0, 0, 7},
-    {VW_FROB, 8, 1, 0},  {VW_FROB, 8, 8, 0},  {VW_FROB, 8, 8, 0},  {VW_MUL, 0, 0, 8}};
+// rounds.
+enum : uint8_t { VW_MUL, VW_CSQR, VW_CONJ, VW_FROB, VW_INV, VW_POWZ, VW_POWS, VW_POWK3, VW_SYNC, VW_END };
+// BN254 easy part f^(p^6 - 1)(p^2 + 1) -> g (slot 1), both waves in step
+__constant__ uint8_t vw_fe_bn[][4] = {{VW_INV, 2, 0, 0},  {VW_CONJ, 1, 0, 0}, {VW_MUL, 1, 1, 2},
+                                      {VW_FROB, 2, 1, 0}, {VW_FROB, 2, 2, 0}, {VW_MUL, 1, 2, 1}};
+// BN254 hard part in u, a = g^u, b = a^u, c = b^u:
+//   f = conj(c^36 b^30 a^18 g^2) (conj(c^36 b^18 a^12) g)^p (b^6 g)^(p^2) g^(p^3),
+// on two waves, each on its own program and slots with per-wave syncs
+// (VW_SYNC: both waves meet).  Wave 0 runs the chain of exponentiations by u
+// (3 x 62 cyclotomic squarings, the critical path); wave 1 meanwhile builds
+// every factor that does not involve c -- during b = a^u the a-chain
+// (a^6, a^12, a^18 = a^12 a^6, shared as in round 5), g^2 and g^(p^3); during
+// c = b^u the b-chain (b^6, b^12, b^18, b^30), X1 = b^30 a^18 g^2,
+// X2 = b^18 a^12 and X34 = (b^6 g)^(p^2) g^(p^3) -- so after c only c^36, two
+// products per wave and one more product remain:
+//   T1 = conj(c^36 X1) X34 (wave 0),  T2 = (conj(c^36 X2) g)^p (wave 1),  f = T1 T2.
+// Slots: 1 g, 4 a, 5 b, 6 c, 7 c^36, 8 T1, 9-14 wave 1's (10 X1, 11 X2, 12 X34, 13 T2).
+__constant__ uint8_t vw_hard_bn[2][34][4] = {
+    {{VW_POWZ, 4, 1, 0}, {VW_SYNC, 0, 0, 0}, {VW_POWZ, 5, 4, 0}, {VW_SYNC, 0, 0, 0}, {VW_POWZ, 6, 5, 0},
+     {VW_SYNC, 0, 0, 0}, {VW_POWS, 7, 6, 36}, {VW_SYNC, 0, 0, 0}, {VW_MUL, 8, 7, 10}, {VW_CONJ, 8, 8, 0},
+     {VW_MUL, 8, 8, 12}, {VW_SYNC, 0, 0, 0}, {VW_MUL, 0, 8, 13}, {VW_SYNC, 0, 0, 0}, {VW_END, 0, 0, 0}},
+    {{VW_SYNC, 0, 0, 0},
+     // a^3 -> 9, a^6 -> 10, a^12 -> 11, a^18 -> 10, g^2 -> 9, a^18 g^2 -> 10, g^(p^3) -> 12
+     {VW_CSQR, 9, 4, 0}, {VW_MUL, 9, 9, 4}, {VW_CSQR, 10, 9, 0}, {VW_CSQR, 11, 10, 0}, {VW_MUL, 10, 11, 10},
+     {VW_CSQR, 9, 1, 0}, {VW_MUL, 10, 10, 9}, {VW_FROB, 12, 1, 0}, {VW_FROB, 12, 12, 0}, {VW_FROB, 12, 12, 0},
+     {VW_SYNC, 0, 0, 0},
+     // b^3 -> 9, b^6 -> 13, b^12 -> 9, b^18 -> 14, b^30 -> 9, X1 -> 10, X2 -> 11, (b^6 g)^(p^2) -> 13, X34 -> 12
+     {VW_CSQR, 9, 5, 0}, {VW_MUL, 9, 9, 5}, {VW_CSQR, 13, 9, 0}, {VW_CSQR, 9, 13, 0}, {VW_MUL, 14, 9, 13},
+     {VW_MUL, 9, 14, 9}, {VW_MUL, 10, 9, 10}, {VW_MUL, 11, 14, 11}, {VW_MUL, 13, 13, 1}, {VW_FROB, 13, 13, 0},
+     {VW_FROB, 13, 13, 0}, {VW_MUL, 12, 13, 12},
+     {VW_SYNC, 0, 0, 0}, {VW_SYNC, 0, 0, 0},
+     {VW_MUL, 13, 7, 11}, {VW_CONJ, 13, 13, 0}, {VW_MUL, 13, 13, 1}, {VW_FROB, 13, 13, 0},
+     {VW_SYNC, 0, 0, 0}, {VW_SYNC, 0, 0, 0}, {VW_END, 0, 0, 0}}};
 // easy part, then BLS12: t = g^K3, t2 = t^(x + p), t3 = t2^(x^2 + p^2 - 1), f = t3 g
 __constant__ uint8_t vw_fe_bls[][4] = {
     {VW_INV, 2, 0, 0},  {VW_CONJ, 1, 0, 0}, {VW_MUL, 1, 1, 2},  {VW_FROB, 2, 1, 0}, {VW_FROB, 2, 2, 0},
@@ -738,20 +767,32 @@ __constant__ uint8_t vw_fe_bls[][4] = {
     {VW_POWZ, 4, 3, 0}, {VW_POWZ, 5, 4, 0}, {VW_FROB, 2, 3, 0}, {VW_FROB, 2, 2, 0}, {VW_MUL, 5, 5, 2},
     {VW_CONJ, 2, 3, 0}, {VW_MUL, 5, 5, 2},  {VW_MUL, 0, 5, 1}};
 
-template <class C>
-KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
+// run nops ops of prog (WS: this wave's own program, per-wave syncs, VW_SYNC
+// a workgroup barrier; else every wave in step)
+template <class C, bool WS>
+KZGX_TW void vw_fe_run(const uint8_t (*prog)[4], int nops, uint32_t slots, uint32_t prod) {
   using P = typename PairOf<C>::T;
   constexpr int E = VWave<C>::E12;
-  const int nops = P::IS_BN ? (int)(sizeof(vw_fe_bn) / 4) : (int)(sizeof(vw_fe_bls) / 4);
+  const int lane = vw_lane<WS>();
   for (int k = 0; k < nops; k++) {
-    const uint8_t* op = P::IS_BN ? vw_fe_bn[k] : vw_fe_bls[k];
+    // the op as uniform (SGPR) values: the program pointer reaches this
+    // non-inlined function in VGPRs, and a switch on a per-lane value would
+    // put the barrier of VW_SYNC under an exec mask (skipped only while the
+    // compiler happens to branch around empty-exec blocks)
+    uint32_t op[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) op[j] = __builtin_amdgcn_readfirstlane((uint32_t)prog[k][j]);
     const uint32_t d = slots + op[1] * E, a = slots + op[2] * E, b = slots + op[3] * E;
     switch (op[0]) {
-      case VW_MUL: vw_mul<C>(d, a, b, prod); break;
-      case VW_CSQR: vw_cyclo_sqr<C>(d, a, prod); break;
-      case VW_CONJ: vw_conj<C>(d, a, threadIdx.x); break;
-      case VW_FROB: vw_frob<C>(d, a, prod); break;
-      case VW_INV: vw_inv_wave<C>(d, a, slots + 7 * E, slots + 8 * E, prod); break;
+      case VW_END: return;
+      case VW_SYNC: __syncthreads(); break;
+      case VW_MUL: vw_mul<C, WS>(d, a, b, prod); break;
+      case VW_CSQR: vw_cyclo_sqr<C, WS>(d, a, prod); break;
+      case VW_CONJ: vw_conj<C, WS>(d, a, lane); break;
+      case VW_FROB: vw_frob<C, WS>(d, a, prod); break;
+      case VW_INV:
+        if constexpr (!WS) vw_inv_wave<C>(d, a, slots + 7 * E, slots + 8 * E, prod);
+        break;
       default: {  // d = a^e (cyclotomic a, top bit of e set), d != a
         uint64_t e0 = op[3], e1 = 0;
         int bits = 32 - __builtin_clz((uint32_t)op[3] | 1u);
@@ -763,15 +804,32 @@ KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
           e1 = P::K3[1];
           bits = P::K3_BITS;
         }
-        vw_copy<C>(d, a);
+        vw_copy<C, WS>(d, a);
 #pragma unroll 1
         for (int i = bits - 2; i >= 0; i--) {
-          vw_cyclo_sqr<C>(d, d, prod);
-          if (((i < 64 ? e0 >> i : e1 >> (i - 64)) & 1ull)) vw_mul<C>(d, d, a, prod);
+          vw_cyclo_sqr<C, WS>(d, d, prod);
+          if (((i < 64 ? e0 >> i : e1 >> (i - 64)) & 1ull)) vw_mul<C, WS>(d, d, a, prod);
         }
-        if (op[0] == VW_POWZ && P::Z_NEG) vw_conj<C>(d, d, threadIdx.x);
+        if (op[0] == VW_POWZ && P::Z_NEG) vw_conj<C, WS>(d, d, lane);
       }
     }
+  }
+}
+
+// The final exponentiation of slot 0 into slot 0.  BN254 needs the block's
+// two waves (k_verify_wave / k_pair2_wave launch 128 threads): the easy part
+// in step, then the hard part on one program per wave (vw_hard_bn).
+template <class C>
+KZGX_TW void vw_final_exp(uint32_t slots, uint32_t prod) {
+  using P = typename PairOf<C>::T;
+  if constexpr (P::IS_BN) {
+    vw_fe_run<C, false>(vw_fe_bn, (int)(sizeof(vw_fe_bn) / 4), slots, prod);
+    // the wave index as a uniform (SGPR) value: each wave's program, and so
+    // every branch around its barriers, is then uniform control flow
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    vw_fe_run<C, true>(vw_hard_bn[w], 34, slots, w ? (uint32_t)VWave<C>::O_PROD2 : prod);
+  } else {
+    vw_fe_run<C, false>(vw_fe_bls, (int)(sizeof(vw_fe_bls) / 4), slots, prod);
   }
 }
 
@@ -1243,30 +1301,40 @@ __global__ __launch_bounds__(128) void k_verify_wave(const uint32_t* __restrict_
   else if (lane == V::I_CINF) in[lane] = commit_inf ? commit_inf[k] : 0u;
   else if (lane == V::I_PINF) in[lane] = proof_inf ? proof_inf[k] : 0u;
   __syncthreads();
-  // ---- [y]G: lane w takes window w's table entry, then a 5-level tree
+  // ---- [y]G on wave 0: lane w takes window w's table entry, then a tree of
+  // group-cooperative additions (coop.hpp, 8 lanes each: 2 + 1 + 1 + 1 + 1
+  // dependent additions, ~4.4 us each against ~8 us for a lone lane's),
+  // synchronised per wave; meanwhile one lane of wave 1 forms
+  // D' = C + [z]pi and pairing 1's scale factors.  Then D = D' - [y]G.
   Affine<C> g;
   const bool gf = affine_from_canonical<C>(g1_0, g);
-  if (lane < 32) {
-    const uint32_t d = (in[V::I_Y + (lane >> 2)] >> (8 * (lane & 3))) & 255u;
-    Xyzz<C> p = xyzz_inf<C>();
-    if (gf && d) p = xyzz_from_affine<C>(affine_load<C>(vtab + ((size_t)lane * 255 + d - 1) * V::AW));
-    xyzz_store<C>(prod + lane * 4 * L, p);
-  }
-  __syncthreads();
-  for (int s = 16; s >= 1; s >>= 1) {
-    if (lane < s)
-      xyzz_store<C>(prod + lane * 4 * L,
-                    xyzz_add<C>(xyzz_load<C>(prod + lane * 4 * L), xyzz_load<C>(prod + (lane + s) * 4 * L)));
-    __syncthreads();
-  }
-  VW_STAMP(1);
-  // ---- D = C - [y]G + [z]pi and the per-pairing scale factors (lane 0)
-  if (lane == 0) {
+  // cooperative scratch: the line area, written only after the prologue
+  uint32_t* sc = vw_smem + V::O_LINES;
+  uint32_t* dp = vw_smem + V::O_SLOT + 2 * V::E12;  // D' then D (XYZZ), a free slot until the Miller loop
+  if (lane < 64) {
+    if (lane < 32) {
+      const uint32_t d = (in[V::I_Y + (lane >> 2)] >> (8 * (lane & 3))) & 255u;
+      Xyzz<C> p = xyzz_inf<C>();
+      if (gf && d) p = xyzz_from_affine<C>(affine_load<C>(vtab + ((size_t)lane * 255 + d - 1) * V::AW));
+      xyzz_store<C>(prod + lane * 4 * L, p);
+    }
+    coop_fence();
+    const int grp = lane >> 3, j = lane & 7;
+    uint32_t* my = sc + grp * COOP_SLOTS * L;
+#pragma unroll 1
+    for (int h = 16; h >= 1; h >>= 1) {
+#pragma unroll 1
+      for (int r = grp; r < h; r += 8) {
+        const Xyzz<C> R = coop_add<C>(xyzz_load<C>(prod + r * 4 * L), xyzz_load<C>(prod + (r + h) * 4 * L), my, j);
+        if (j == 0) xyzz_store<C>(prod + r * 4 * L, R);
+      }
+      coop_fence();
+    }
+  } else if (lane == 64) {
     Affine<C> c, pi;
     const bool cf = affine_from_canonical<C>(in + V::I_C, c) && !in[V::I_CINF];
     const bool pf = affine_from_canonical<C>(in + V::I_P, pi) && !in[V::I_PINF];
-    Xyzz<C> d = xyzz_neg<C>(xyzz_load<C>(prod));
-    if (cf) d = xyzz_add_affine<C>(d, c);
+    Xyzz<C> d = cf ? xyzz_from_affine<C>(c) : xyzz_inf<C>();
     if (pf) {
       int top = -1;
       for (int b = 255; b >= 0 && top < 0; b--)
@@ -1278,17 +1346,29 @@ __global__ __launch_bounds__(128) void k_verify_wave(const uint32_t* __restrict_
       }
       d = xyzz_add<C>(d, zp);
     }
-    const bool df = !xyzz_is_inf<C>(d);
-    // pairing 0: (-D, G2[0]) with line factors (-Y ZZ, X ZZZ, ZZ ZZZ)
-    vw_st<C>(scale + 0 * L, fp_neg<F>(f29_mul<F>(d.Y, d.ZZ)));
-    vw_st<C>(scale + 1 * L, f29_mul<F>(d.X, d.ZZZ));
-    vw_st<C>(scale + 2 * L, f29_mul<F>(d.ZZ, d.ZZZ));
+    xyzz_store<C>(dp, d);
     // pairing 1: (pi, G2[1]) with (y, x, 1)
     vw_st<C>(scale + 3 * L, pi.y);
     vw_st<C>(scale + 4 * L, pi.x);
     vw_st<C>(scale + 5 * L, f29_one<F>());
-    flag[0] = (df && qfin[0]) ? 1u : 0u;
     flag[1] = (pf && qfin[1]) ? 1u : 0u;
+  }
+  __syncthreads();
+  VW_STAMP(1);
+  // ---- D = D' - [y]G (group 0, cooperative), then pairing 0's line factors
+  // for (-D, G2[0]): (-Y ZZ, X ZZZ, ZZ ZZZ), one product per lane
+  if (lane < 8) {
+    const Xyzz<C> R = coop_add<C>(xyzz_load<C>(dp), xyzz_neg<C>(xyzz_load<C>(prod)), sc, lane);
+    if (lane == 0) xyzz_store<C>(dp, R);
+    coop_fence();
+    if (lane < 3) {
+      const Xyzz<C> d = xyzz_load<C>(dp);
+      const F29<F> x = lane == 0 ? d.Y : lane == 1 ? d.X : d.ZZ;
+      const F29<F> y = lane == 0 ? d.ZZ : d.ZZZ;
+      const F29<F> v = f29_mul<F>(x, y);
+      vw_st<C>(scale + lane * L, lane == 0 ? fp_neg<F>(v) : v);
+      if (lane == 0) flag[0] = (!xyzz_is_inf<C>(d) && qfin[0]) ? 1u : 0u;
+    }
   }
   __syncthreads();
   VW_STAMP(2);
