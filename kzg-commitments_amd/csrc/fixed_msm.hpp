@@ -431,6 +431,35 @@ __global__ __launch_bounds__(64, fixed_accum_waves<C>()) void k_fixed_accum_flat
   if (threadIdx.x == 0) xyzz_store<C>(part + ((size_t)b * (T / 64) + t / 64) * XW, acc);
 }
 
+// One fold level as its own launch (the default; KZGX_FOLD3_SPLIT=0 runs
+// k_fixed_fold3's arrival counters and device-scope fences): wavefront g
+// folds in[g per, g per + per) into out[g]; with fin, group g = MSM b's last
+// level, stored as the XYZZ record or converted to affine
+template <class C>
+__global__ __launch_bounds__(64) void k_fold_level(const uint32_t* __restrict__ in, uint32_t per,
+                                                   uint32_t* __restrict__ out, int fin, uint32_t* __restrict__ fout,
+                                                   uint32_t* __restrict__ fout_inf, uint32_t* __restrict__ xyzz_out) {
+  constexpr int XW = xyzz_words<C>();
+  const uint32_t g = blockIdx.x, lane = threadIdx.x;
+  const uint32_t* src = in + (size_t)g * per * XW;
+  Xyzz<C> s;
+  if (per == 256) {
+    auto ld = [&](int k) { return xyzz_load<C>(src + (size_t)(lane + 64 * k) * XW); };
+    s = xyzz_wave_sum<C>(xyzz_add_impl<C>(xyzz_add_impl<C>(ld(0), ld(1)), xyzz_add_impl<C>(ld(2), ld(3))), lane, true);
+  } else {
+    s = lat_fold<C>(src, per, lane, true);
+  }
+  if (!fin) {
+    if (lane == 0) xyzz_store<C>(out + (size_t)g * XW, s);
+    return;
+  }
+  if (xyzz_out) {
+    if (lane == 0) xyzz_store<C>(xyzz_out + (size_t)g * XW, s);
+    return;
+  }
+  lat_store_affine<C>(s, g, lane, fout, fout_inf);
+}
+
 // The flat path's reduction in one launch (three fold levels, arrival
 // counters as k_fixed_accum_lat): wavefront q < P1 of MSM b folds partials
 // [q per, q per + per) (lat_fold: strided sums, then the butterfly with
@@ -585,6 +614,25 @@ int fixed_msm_win(Ctx* ctx, FixedTable& ft, const uint32_t* d_scalars, size_t n,
                              (uint32_t)n, stride_words, ft.d, tab_strides<C>(ft), fixed_inf(ft), Q, T, ws.fpart, 1u);
         }
         ProfScope p(ctx, st, "msm_reduce");
+        // three launches by default: measured 15-20 us faster than
+        // k_fixed_fold3's one launch on the same box (131 073 points, c = 10:
+        // 0.438-0.458 vs 0.461-0.480 ms, profiles/r06_shard_fixed.jsonl) --
+        // the arrival pattern's device-scope release fences write back the
+        // L2 that still holds the accumulation's 28 MB of partials, where a
+        // kernel boundary does it once.  KZGX_FOLD3_SPLIT=0: k_fixed_fold3 (A/B)
+        static const bool split = !(std::getenv("KZGX_FOLD3_SPLIT") && std::getenv("KZGX_FOLD3_SPLIT")[0] == '0');
+        if (split && per == 256 && P1 % 64 == 0) {
+          uint32_t* f1 = ws.fsum;
+          uint32_t* f2 = ws.fsum + batch * (size_t)P1 * xyzz_words<C>();
+          hipLaunchKernelGGL(k_fold_level<C>, dim3(batch * P1), dim3(64), 0, st, ws.fpart, 256u, f1, 0, nullptr,
+                             nullptr, nullptr);
+          hipLaunchKernelGGL(k_fold_level<C>, dim3(batch * NG), dim3(64), 0, st, f1, 64u, f2, 0, nullptr, nullptr,
+                             nullptr);
+          hipLaunchKernelGGL(k_fold_level<C>, dim3(batch), dim3(64), 0, st, f2, NG, nullptr, 1, d_out, d_out_inf,
+                             xyzz_out);
+          KZGX_TRY_HIP(hipGetLastError());
+          return KZGX_OK;
+        }
         hipLaunchKernelGGL(k_fixed_fold3<C>, dim3(P1, (unsigned)batch), dim3(64), 0, st, ws.fpart, per, P1, NG,
                            ws.fsum, ws.fsum + batch * (size_t)P1 * xyzz_words<C>(), ws.lat_cnt, d_out, d_out_inf,
                            xyzz_out);
