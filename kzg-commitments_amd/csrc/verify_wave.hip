@@ -232,12 +232,13 @@ KZGX_DEV F29<F> lin_fin(const LinAcc<F>& a) {
   constexpr int L = F::L;
   const double x = (double)a.v[L - 1] * LinInvM<F>::T0 + (double)a.v[L - 2] * LinInvM<F>::T1 +
                    (double)a.v[L - 3] * LinInvM<F>::T2;
-  const int64_t q = (int64_t)__builtin_floor(x - 0x1p-12);
+  // |q| < 2^20: one v_mad_i64_i32 per limb, off the carry chain
+  const int32_t q = (int32_t)__builtin_floor(x - 0x1p-12);
   F29<F> r;
   int64_t c = 0;
 #pragma unroll
   for (int l = 0; l < L; l++) {
-    const int64_t s = a.v[l] - q * (int64_t)F::P[l] + c;
+    const int64_t s = (a.v[l] - (int64_t)q * (int64_t)(int32_t)F::P[l]) + c;
     if (l + 1 < L) {
       r.v[l] = (uint32_t)s & M29;
       c = s >> 29;  // arithmetic
@@ -246,6 +247,23 @@ KZGX_DEV F29<F> lin_fin(const LinAcc<F>& a) {
     }
   }
   return r;
+}
+
+// The fold of an output split over two adjacent lanes (lane ^ 1): each
+// accumulates its share of the terms, then a += the partner's accumulator by
+// DPP (quad_perm [1, 0, 3, 2]: a VALU operand modifier, no LDS), so the
+// lin_fin lane's dependent limb-sum chains are half as long.
+KZGX_DEV uint32_t dpp_xor1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+template <class F>
+KZGX_DEV void lin_pair_sum(LinAcc<F>& a) {
+#pragma unroll
+  for (int l = 0; l < F::L; l++) {
+    const uint64_t u = (uint64_t)a.v[l];
+    const uint64_t o = ((uint64_t)dpp_xor1((uint32_t)(u >> 32)) << 32) | dpp_xor1((uint32_t)u);
+    a.v[l] += (int64_t)o;
+  }
 }
 
 // Karatsuba parts of an Fp2 product x y: 0 = xa ya, 1 = xb yb,
@@ -353,18 +371,21 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
     }
   }
   vw_sync<WS>();
-  if (lane < 12) {
-    // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij
-    const int k = lane >> 1, im = lane & 1;
+  if (lane < 24) {
+    // c_k = sum_{i+j=k} p_ij + xi sum_{i+j=k+6} p_ij; lanes 2 o, 2 o + 1
+    // take i = h, h + 2, h + 4 (h = lane & 1) of output o = (k, im)
+    const int o = lane >> 1, h = lane & 1, k = o >> 1, im = o & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
+    for (int i2 = 0; i2 < 3; i2++) {
+      const int i = 2 * i2 + h;
       const bool wrap = i > k;
       const int j = wrap ? k + 6 - i : k - i;
       lin_add_f2p<F, PL>(acc, prod + (i * 6 + j) * 3 * PL, im, wrap, 1);
     }
-    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+    lin_pair_sum<F>(acc);
+    if (!h) vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
   vw_sync<WS>();
 }
@@ -386,6 +407,7 @@ KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o, int la
   }
   __syncthreads();
   if (lane < 12) {
+    // (three terms: a two-lane split measured slower, 2.29 vs 1.98 us)
     const int k = lane >> 1, im = lane & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
@@ -424,22 +446,25 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o, int lane) {
     vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(a + (i + idx) * E2), lane % 3));
   }
   __syncthreads();
-  if (lane < 12) {
+  if (lane < 24) {
     // c_k = sum_i a_i a_{(k - i) mod 6} (xi for the wrapped ones): one
     // uniform pass over i, reading the unordered pair's parts -- a cross
     // pair (i, j) is met at i and at j, so it counts twice (the lanes'
-    // divergent walk over i <= j executed the union: twice the loads)
-    const int k = lane >> 1, im = lane & 1;
+    // divergent walk over i <= j executed the union: twice the loads).
+    // Lanes 2 o, 2 o + 1 of output o = (k, im) take i = h, h + 2, h + 4.
+    const int o = lane >> 1, h = lane & 1, k = o >> 1, im = o & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
+    for (int i2 = 0; i2 < 3; i2++) {
+      const int i = 2 * i2 + h;
       const bool wrap = i > k;
       const int j = wrap ? k + 6 - i : k - i;
       const int lo = i < j ? i : j, hi = i < j ? j : i;
       lin_add_f2p<F, PL>(acc, prod + 3 * vw_pair_index<C>(lo, hi) * PL, im, wrap, 1);
     }
-    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+    lin_pair_sum<F>(acc);
+    if (!h) vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
   __syncthreads();
 }
@@ -471,14 +496,16 @@ KZGX_DEV F29<F> vw_norm(const uint32_t (&o)[F::L]) {
   }
   return r;
 }
-template <class C, bool WS = false>
+// PH (measurement only, k_vw_bench): 1 = the product round alone, 2 = the
+// fold round alone, 3 = the op
+template <class C, bool WS = false, int PH = 3>
 KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
   uint32_t *dst = vw_smem + dst_o, *prod = vw_smem + prod_o;
   const uint32_t* a = vw_smem + a_o;
   const int lane = vw_lane<WS>();
-  if (lane < 18) {
+  if ((PH & 1) && lane < 18) {
     const int j = lane / 6, which = (lane / 3) & 1, part = lane % 3;
     const uint32_t *xp = a + j * E2, *yp = a + (j + 3) * E2;
     // part 0: (re, re), 1: (im, im), 2: (re + im, re + im) of
@@ -497,8 +524,9 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     vw_stp<C>(prod + lane * PL, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
   }
   vw_sync<WS>();
-  if (lane < 12) {
-    const int k = lane >> 1, im = lane & 1;
+  if ((PH & 2) && lane < 24) {
+    // lanes 2 o, 2 o + 1 of output o = (k, im): the t parts / the u parts and 2 a_k
+    const int o = lane >> 1, h = lane & 1, k = o >> 1, im = o & 1;
     const int j = (k & 1) ? (k == 3 ? 0 : k == 5 ? 1 : 2) : (k >> 1);
     const uint32_t* q = prod + j * 6 * PL;
     int cp0, cp1, cp2, cq0 = 0, cq1 = 0, cq2 = 0;
@@ -518,16 +546,18 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
       cp1 = im ? -4 : 0;
       cp2 = im ? 2 : -2;
     }
+    // one instruction stream for both halves (selected addresses and
+    // coefficients: an if / else on h would run both sides masked); the
+    // h = 0 lane adds a_k with coefficient 0
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_addp<F>(acc, q, 3 * cp0);
-    lin_addp<F>(acc, q + PL, 3 * cp1);
-    lin_addp<F>(acc, q + 2 * PL, 3 * cp2);
-    lin_addp<F>(acc, q + 3 * PL, 3 * cq0);
-    lin_addp<F>(acc, q + 4 * PL, 3 * cq1);
-    lin_addp<F>(acc, q + 5 * PL, 3 * cq2);
-    lin_add<F>(acc, a + k * E2 + im * L, (k & 1) ? 2 : -2);
-    vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
+    const uint32_t* qh = q + 3 * h * PL;
+    lin_addp<F>(acc, qh, 3 * (h ? cq0 : cp0));
+    lin_addp<F>(acc, qh + PL, 3 * (h ? cq1 : cp1));
+    lin_addp<F>(acc, qh + 2 * PL, 3 * (h ? cq2 : cp2));
+    lin_add<F>(acc, a + k * E2 + im * L, h ? ((k & 1) ? 2 : -2) : 0);
+    lin_pair_sum<F>(acc);
+    if (!h) vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
   vw_sync<WS>();
 }
@@ -1430,7 +1460,10 @@ __global__ __launch_bounds__(64) void k_vw_bench(int op, uint32_t iters, uint64_
       case 3: vw_mul_line<C>(s0, V::O_LINES, V::O_PROD, lane); break;
       case 4: vw_frob<C>(s0, s0, V::O_PROD); break;
       case 5: vw_inv<C>(s1, s0); break;
-      default: vw_inv_wave<C>(s1, s0, s1 + V::E12, s1 + 2 * V::E12, V::O_PROD); break;
+      case 6: vw_inv_wave<C>(s1, s0, s1 + V::E12, s1 + 2 * V::E12, V::O_PROD); break;
+      case 7: vw_cyclo_sqr<C, true, 1>(s0, s0, V::O_PROD); break;  // product round, per-wave sync
+      case 8: vw_cyclo_sqr<C, true, 2>(s0, s0, V::O_PROD); break;  // fold round, per-wave sync
+      default: vw_cyclo_sqr<C, true, 3>(s0, s0, V::O_PROD); break;  // 9: the op, per-wave sync
     }
   }
   const uint64_t w1 = wall_clock64(), c1 = clock64();

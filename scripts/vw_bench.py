@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import kzgx  # noqa: E402
 import kzg_ref as K  # noqa: E402
 
-OPS = ["cyclo_sqr", "mul", "sqr", "mul_line", "frob", "inv", "inv_wave"]
+OPS = ["cyclo_sqr", "mul", "sqr", "mul_line", "frob", "inv", "inv_wave", "csqr_product_ws", "csqr_fold_ws", "csqr_ws"]
 
 
 def main():
