@@ -498,6 +498,34 @@ KZGX_DEV F29<F> vw_norm(const uint32_t (&o)[F::L]) {
 }
 // PH (measurement only, k_vw_bench): 1 = the product round alone, 2 = the
 // fold round alone, 3 = the op
+// one carry step for every limb at once (no chain): limbs < 2^32 in, limbs
+// < 2^29 + 8 out (the top limb absorbs), the value unchanged.  f29_mul's
+// column sums stay < 2^62 with such limbs; the product's bound depends only
+// on the values (< 10 m here).
+template <class F>
+KZGX_DEV F29<F> vw_norm1(const uint32_t (&o)[F::L]) {
+  F29<F> r;
+  r.v[0] = o[0] & M29;
+#pragma unroll
+  for (int l = 1; l < F::L; l++) r.v[l] = (l + 1 < F::L ? (o[l] & M29) : o[l]) + (o[l - 1] >> 29);
+  return r;
+}
+// L limbs from LDS with 64-bit accesses: ODD = the first limb sits at an odd
+// word (slots and coefficients start at even words; the imaginary part of an
+// Fp2 at +L)
+template <int L, bool ODD>
+KZGX_DEV void vw_ld_limbs(const uint32_t* p, uint32_t (&v)[L]) {
+  constexpr int S = ODD ? 1 : 0;
+  if (ODD) v[0] = p[0];
+#pragma unroll
+  for (int i = 0; S + 2 * i + 1 < L; i++) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p + S + 2 * i);
+    v[S + 2 * i] = t.x;
+    v[S + 2 * i + 1] = t.y;
+  }
+  if ((L - S) & 1) v[L - 1] = p[L - 1];
+}
+
 template <class C, bool WS = false, int PH = 3>
 KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
   using F = typename C::Fp29;
@@ -512,16 +540,20 @@ KZGX_DEV void vw_cyclo_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o) {
     // t: (x, y);  u: (x + y, x + xi y), x + xi y = (xa + ya - yb, xb + ya + yb)
     const uint32_t e0 = part != 1 ? ~0u : 0u, e1 = part != 0 ? ~0u : 0u, w = which ? ~0u : 0u;
     const uint32_t y2 = part == 2 ? ~0u : 0u, yn = part == 0 ? ~0u : 0u, yp1 = part == 1 ? ~0u : 0u;
-    uint32_t o0[L], o1[L];
+    uint32_t o0[L], o1[L], XA[L], XB[L], YA[L], YB[L];
+    vw_ld_limbs<L, false>(xp, XA);
+    vw_ld_limbs<L, (L & 1) != 0>(xp + L, XB);
+    vw_ld_limbs<L, false>(yp, YA);
+    vw_ld_limbs<L, (L & 1) != 0>(yp + L, YB);
 #pragma unroll
     for (int l = 0; l < L; l++) {
-      const uint32_t xa = xp[l], xb = xp[L + l], ya = yp[l], yb = yp[L + l];
+      const uint32_t xa = XA[l], xb = XB[l], ya = YA[l], yb = YB[l];
       const uint32_t sx = (xa & e0) + (xb & e1), sy = (ya & e0) + (yb & e1);
       o0[l] = sx + (sy & w);
       const uint32_t u1 = sx + ya + (ya & y2) + ((F::P2B[l] - yb) & yn) + (yb & yp1);
       o1[l] = which ? u1 : sy;
     }
-    vw_stp<C>(prod + lane * PL, f29_mul<F>(vw_norm<F>(o0), vw_norm<F>(o1)));
+    vw_stp<C>(prod + lane * PL, f29_mul<F>(vw_norm1<F>(o0), vw_norm1<F>(o1)));
   }
   vw_sync<WS>();
   if ((PH & 2) && lane < 24) {
