@@ -938,6 +938,18 @@ def main():
     ctx.close()
 
 
+def cfg5_fixed_bits(requested, shard_points):
+    """configs[4]'s fixed-base window for one rank's shard: --fixed-bits when
+    given (>= 0), else c = 10 for shards of <= 2^18 + 1 points (4 ranks and
+    more: 0.44 ms per 131 073-point partial against 0.68 ms table-free,
+    0.74 against 1.0 ms at 262 145 points) and 0 (the wide-window Pippenger)
+    for larger ones.  set_fixed_with_fallback then steps the window down to
+    what fits."""
+    if requested >= 0:
+        return requested
+    return 10 if shard_points <= (1 << 18) + 1 else 0
+
+
 def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     """configs[4]: one BN254 degree-2^20 commitment sharded over the ranks.
     Each rank owns a contiguous point range with its own SRS slice; the only
@@ -968,7 +980,7 @@ def run_cfg5(args, world, rank, local, dev, torch, dist, kzgx):
     # profiles/r06_shard_fixed.jsonl); larger shards stay table-free (2^20 + 1
     # points: c = 8 would run 3.05 ms against 2.05 ms).
     t_setup = time.perf_counter()
-    fixed_bits = args.fixed_bits if args.fixed_bits >= 0 else (10 if count <= (1 << 18) + 1 else 0)
+    fixed_bits = cfg5_fixed_bits(args.fixed_bits, count)
     if fixed_bits:
         fixed_bits = set_fixed_with_fallback(kzgx, ctx, fixed_bits, max(count, 1),
                                              budget=args.table_gb * 1e9 if args.table_gb > 0 else None)

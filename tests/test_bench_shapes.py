@@ -33,3 +33,21 @@ def test_bench_inputs_shapes():
     assert c.shape == (1, 33, 4)
     ints = [sum(int(w) << (64 * i) for i, w in enumerate(row)) for row in c[0]]
     assert all(0 <= v < C.r for v in ints)
+
+
+def test_cfg5_fixed_bits_choice():
+    """configs[4]: a rank's shard of <= 2^18 + 1 points gets the c = 10
+    fixed-base table unless --fixed-bits says otherwise (bench.cfg5_fixed_bits;
+    kzgx_dist.shard_range gives the shard sizes of the 2^20 + 1 coefficients)"""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "kzg-commitments_amd", "python"))
+    import bench
+    import kzgx_dist
+    n = (1 << 20) + 1
+    want = {1: 0, 2: 0, 4: 10, 8: 10}
+    for world, c in want.items():
+        counts = [kzgx_dist.shard_range(n, world, r)[1] for r in range(world)]
+        assert sum(counts) == n
+        assert {bench.cfg5_fixed_bits(-1, k) for k in counts} == {c}, world
+    assert bench.cfg5_fixed_bits(0, 131073) == 0
+    assert bench.cfg5_fixed_bits(8, (1 << 20) + 1) == 8
