@@ -193,7 +193,7 @@ def test_fixed_large_single_msm(name, C, batch, fresh_ctx):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
-@pytest.mark.parametrize("tau_kind,batch", [("default", 1), ("default", 2), ("zero", 1)])
+@pytest.mark.parametrize("tau_kind,batch", [("default", 1), ("default", 2), ("default", 5), ("zero", 1)])
 def test_fixed_flat_terms(name, C, tau_kind, batch, fresh_ctx):
     """few large MSMs with >= 32 digit terms per resident lane take the
     flattened-term kernel (k_fixed_accum_flat): threads start inside a point
@@ -201,7 +201,10 @@ def test_fixed_flat_terms(name, C, tau_kind, batch, fresh_ctx):
     boundary, and tau = 0 makes every SRS point but the first infinity (all of
     its terms skipped).  c = 4: 64 windows, 100 003 points -> 33 terms per
     thread; scalars with digit edge cases sit on both sides of thread
-    boundaries."""
+    boundaries.  The reduction: batches 1 and 2 take the three fold launches
+    (k_fold_level, 768 / 384 first-level wavefronts per MSM), batch 5 the
+    one-launch arrival-counter form (k_fixed_fold3: 144 per MSM, not a
+    multiple of 64)."""
     ctx = fresh_ctx(name)
     tau = K.default_tau(C) if tau_kind == "default" else 0
     n, c = 100003, 4
