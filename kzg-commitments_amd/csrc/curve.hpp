@@ -445,6 +445,31 @@ KZGX_PT bool xyzz_to_affine_lane(const Xyzz<C>& p, Affine<C>& out) {
   return xyzz_to_affine_impl<C, true>(p, out);
 }
 
+// XYZZ -> the canonical affine words written at out (x || y, C::Fp::N words
+// each, zeros for infinity), for the final result of a latency path: one
+// lane's point converted by the whole wave (uniform inversion, as
+// xyzz_to_affine_lane).  The inverse comes out as the plain residue
+// i = 1 / (ZZ ZZZ) (f29_inv_uniform_raw), so 1/ZZ = i ZZZ / R and
+// x = X (1/ZZ) / R are already canonical: against xyzz_to_affine_lane +
+// affine_to_canonical, one product by R^2 and the two from-Montgomery
+// products leave the chain.  Every lane computes; the caller lets one store.
+template <class C>
+KZGX_PT bool xyzz_to_canonical_lane(const Xyzz<C>& p, uint32_t (&wx)[C::Fp::N], uint32_t (&wy)[C::Fp::N]) {
+  using F = typename C::Fp29;
+  constexpr int N = C::Fp::N;
+  if (xyzz_is_inf<C>(p)) {
+#pragma unroll
+    for (int k = 0; k < N; k++) wx[k] = wy[k] = 0u;
+    return false;
+  }
+  const F29<F> i = f29_inv_uniform_raw<F, N>(f29_mul<F>(p.ZZ, p.ZZZ), C::Fp::P);
+  const F29<F> izz = f29_mul<F>(i, p.ZZZ);   // 1 / ZZ, plain
+  const F29<F> izzz = f29_mul<F>(i, p.ZZ);   // 1 / ZZZ, plain
+  f29_to_words<F, N>(f29_reduce<F>(f29_mul<F>(p.X, izz)), wx);
+  f29_to_words<F, N>(f29_reduce<F>(f29_mul<F>(p.Y, izzz)), wy);
+  return true;
+}
+
 // ---- storage ---------------------------------------------------------------
 // table / workspace affine point: x (L words) || y (L words), padded to
 // affine_words<C>() so every point starts 16-byte aligned

@@ -950,7 +950,7 @@ __device__ __noinline__ F29<F> f29_inv(const F29<F>& a, const uint32_t (&pm2)[NW
 // with lanes 0-3 active the four linear combinations of a pass run one per
 // lane (combine4).  Never with a different value per lane (the batched
 // finish kernels).
-template <class F, int NW, bool U = false>
+template <class F, int NW, bool U = false, bool RAW = false>
 __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[NW]) {
   constexpr int L = F::L;
   constexpr int K = 29;
@@ -1136,6 +1136,8 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[
     b = b2;
   }
   const F29<F> r2 = f29_const<F>(F::R2);
+  // RAW: (y / R)^-1 as a plain residue, v R = one product by R^2
+  if constexpr (RAW) return f29_mul<F>(v, r2);
   return f29_mul<F>(f29_mul<F>(v, r2), r2);
 }
 
@@ -1143,6 +1145,12 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[
 template <class F, int NW>
 KZGX_DEV F29<F> f29_inv_uniform(const F29<F>& a, const uint32_t (&m)[NW]) {
   return f29_inv_vt<F, NW, true>(a, m);
+}
+// the same inverse of the Montgomery value a (= A R) as the plain residue
+// A^-1 (not its Montgomery form A^-1 R): one product fewer
+template <class F, int NW>
+KZGX_DEV F29<F> f29_inv_uniform_raw(const F29<F>& a, const uint32_t (&m)[NW]) {
+  return f29_inv_vt<F, NW, true, true>(a, m);
 }
 
 // the inversion the finish / pairing paths use (KZGX_INV_FERMAT: the

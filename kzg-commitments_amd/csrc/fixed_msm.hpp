@@ -320,10 +320,15 @@ KZGX_DEV void lat_store_affine(const Xyzz<C>& acc, uint32_t b, uint32_t lane, ui
     s.ZZ.v[k] = __builtin_amdgcn_readfirstlane(acc.ZZ.v[k]);
     s.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(acc.ZZZ.v[k]);
   }
-  Affine<C> a;
-  const bool fin = xyzz_to_affine_lane<C>(s, a);
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  const bool fin = xyzz_to_canonical_lane<C>(s, wx, wy);
   if (lane == 0) {
-    affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      out[(size_t)b * 2 * N + k] = wx[k];
+      out[(size_t)b * 2 * N + N + k] = wy[k];
+    }
     out_inf[b] = fin ? 0u : 1u;
   }
 }

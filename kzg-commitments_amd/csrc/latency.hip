@@ -113,10 +113,14 @@ __global__ __launch_bounds__(64) void k_g1_fold_xyzz(const uint32_t* __restrict_
     const Xyzz<C> x = xyzz_shfl_down_w<C>(acc, (int)(8 * o));
     if (g < o) acc = coop_add<C>(acc, x, my, j);
   }
-  Affine<C> a;
-  const bool fin = xyzz_to_affine_impl<C, true>(acc, a);  // lane 0's value (group 0: the sum)
+  uint32_t wx[N], wy[N];
+  const bool fin = xyzz_to_canonical_lane<C>(acc, wx, wy);  // lane 0's value (group 0: the sum)
   if (lane == 0) {
-    affine_to_canonical<C>(out, a, fin);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      out[k] = wx[k];
+      out[N + k] = wy[k];
+    }
     out[2 * N] = fin ? 0u : 1u;
     out[2 * N + 1] = 0u;
   }
@@ -403,10 +407,15 @@ __global__ __launch_bounds__(64) void k_coop_finish(const uint32_t* __restrict__
     if (threadIdx.x == 0) xyzz_store<C>(xyzz_out, V);
     return;
   }
-  Affine<C> a;
-  const bool fin = xyzz_to_affine_impl<C, true>(V, a);
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  const bool fin = xyzz_to_canonical_lane<C>(V, wx, wy);
   if (threadIdx.x != 0) return;
-  affine_to_canonical<C>(out, a, fin);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    out[k] = wx[k];
+    out[N + k] = wy[k];
+  }
   *out_inf = fin ? 0u : 1u;
 }
 
