@@ -1135,10 +1135,10 @@ __device__ __noinline__ F29<F> f29_inv_vt(const F29<F>& in_, const uint32_t (&)[
     a = a2;
     b = b2;
   }
-  const F29<F> r2 = f29_const<F>(F::R2);
-  // RAW: (y / R)^-1 as a plain residue, v R = one product by R^2
-  if constexpr (RAW) return f29_mul<F>(v, r2);
-  return f29_mul<F>(f29_mul<F>(v, r2), r2);
+  // RAW: (y / R)^-1 as a plain residue, v R = one product by R^2; else its
+  // Montgomery form v R^2 = one product by R^3 (was two by R^2)
+  if constexpr (RAW) return f29_mul<F>(v, f29_const<F>(F::R2));
+  return f29_mul<F>(v, f29_const<F>(F::R3));
 }
 
 // a^-1 of the first active lane's a (see U above)

@@ -86,6 +86,7 @@ def field29(name, m, L):
                  ", ".join("0x%08xu" % v for v in b))
     lines += [
         "  static constexpr uint32_t R2[L] = %s;  // R^2 mod m" % arr29(R * R % m, L),
+        "  static constexpr uint32_t R3[L] = %s;  // R^3 mod m" % arr29(R * R * R % m, L),
         "  static constexpr uint32_t ONE[L] = %s;  // R mod m" % arr29(R % m, L),
         "  // low limb of k m, k = 0..3 (zero filter for values < 4m)",
         "  static constexpr uint32_t LOW[4] = {0u, 0x%08xu, 0x%08xu, 0x%08xu};" % tuple(

@@ -626,10 +626,15 @@ __global__ __launch_bounds__(FOLD_WG) void k_msm_bucket_fold_wg(const uint32_t* 
     s.ZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZ.v[k]);
     s.ZZZ.v[k] = __builtin_amdgcn_readfirstlane(U.ZZZ.v[k]);
   }
-  Affine<C> a;
-  const bool fin = xyzz_to_affine_lane<C>(s, a);
+  constexpr int N = C::Fp::N;
+  uint32_t wx[N], wy[N];
+  const bool fin = xyzz_to_canonical_lane<C>(s, wx, wy);
   if (l != 0) return;
-  affine_to_canonical<C>(out + (size_t)b * 2 * C::Fp::N, a, fin);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    out[(size_t)b * 2 * N + k] = wx[k];
+    out[(size_t)b * 2 * N + N + k] = wy[k];
+  }
   out_inf[b] = fin ? 0u : 1u;
 }
 
@@ -667,9 +672,14 @@ __global__ __launch_bounds__(256) void k_xyzz_sum(const uint32_t* __restrict__ p
     __syncthreads();
   }
   if (t == 0) {
-    Affine<C> a;
-    bool fin = xyzz_to_affine_lane<C>(acc, a);
-    affine_to_canonical<C>(out, a, fin);
+    constexpr int N = C::Fp::N;
+    uint32_t wx[N], wy[N];
+    const bool fin = xyzz_to_canonical_lane<C>(acc, wx, wy);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      out[k] = wx[k];
+      out[N + k] = wy[k];
+    }
     *out_inf = fin ? 0u : 1u;
   }
 }
