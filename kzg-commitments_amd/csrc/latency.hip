@@ -543,10 +543,10 @@ template <class C>
 static int big_reduce_impl(const uint32_t* d_offsets, uint32_t nb, const uint32_t* d_bsum, uint32_t* d_rt,
                            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st, uint32_t* xyzz_out) {
   const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
-  if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb in [512, 2^15]
+  if (NG < 1 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;  // nb >= 512
 #ifdef KZGX_AB_VARIANTS
   static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
-  if (lone && !xyzz_out) {
+  if (lone && !xyzz_out && NG <= 64) {  // k_lat_fold2: one wave over the NG groups
     uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
     hipLaunchKernelGGL((k_lat_bucket_sums<C, BIG_RED_J>), dim3((T1 + 255) / 256), dim3(256), 0, st, d_offsets, nb,
                        d_bsum, d_rt);
@@ -646,7 +646,7 @@ static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint
                                const uint32_t* d_flag, uint32_t* d_rt, uint32_t* d_out, uint32_t* d_out_inf,
                                hipStream_t st, uint32_t* xyzz_out) {
   const uint32_t T1 = nb / BIG_RED_J, NG = T1 / BIG_F1;
-  if (NG < 1 || NG > 64 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;
+  if (NG < 1 || T1 % BIG_F1) return KZGX_ERR_INTERNAL;
   uint32_t* vt = d_rt + (size_t)T1 * 2 * xyzz_words<C>();
   // pre-sum passes: as many as the largest possible bucket (s_ub partials)
   // could need; each exits at once unless some bucket has > LAT_MAXSEG
@@ -664,7 +664,7 @@ static int big_reduce_seg_impl(const uint32_t* d_seg_off, uint32_t* d_part, uint
   // the lone-lane k_lat_fold1 / k_lat_fold2, A/B)
 #ifdef KZGX_AB_VARIANTS
   static const bool lone = std::getenv("KZGX_BIG_LONEFOLD") != nullptr;
-  if (lone && !xyzz_out) {
+  if (lone && !xyzz_out && NG <= 64) {  // k_lat_fold2: one wave over the NG groups
     hipLaunchKernelGGL(k_lat_fold1<C>, dim3(2 * NG), dim3(BIG_F1), 0, st, d_rt, NG, vt);
     hipLaunchKernelGGL(k_lat_fold2<C>, dim3(1), dim3(64), 0, st, vt, NG, d_out, d_out_inf);
     KZGX_TRY_HIP(hipGetLastError());

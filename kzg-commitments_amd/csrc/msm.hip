@@ -848,7 +848,10 @@ template <int CB>
 struct BigFine {
   static constexpr uint32_t NF = Win<CB>::NB / BIG_NC;  // buckets per coarse bin
   static constexpr int FB = CB - 1 - 10;
-  static_assert(NF >= 2 && NF <= 32 && (1u << FB) == NF, "c = 12..16");
+  static_assert(NF >= 2 && NF <= 64 && (1u << FB) == NF, "c = 12..17");
+  // a pass-1 entry: table index (IDX bits) | fine bits << IDX | sign << 31:
+  // 26 index bits up to c = 16, 25 at c = 17 (its 6 fine bits)
+  static constexpr uint32_t IDX = FB <= 5 ? BIG_IDX_BITS : 31u - (uint32_t)FB;
 };
 
 template <int CB>
@@ -988,7 +991,7 @@ __global__ __launch_bounds__(BIG_TPB) void k_big2_scatter(const uint32_t* __rest
       if (d != 0) {
         const uint32_t bk = (uint32_t)(d < 0 ? -d : d) - 1;
         const uint32_t pos = atomicAdd(&lcur[bk >> FB], 1u);
-        stage[pos] = ((uint32_t)w * n_rows + i) | ((bk & FM) << BIG_IDX_BITS) | (d < 0 ? 0x80000000u : 0u);
+        stage[pos] = ((uint32_t)w * n_rows + i) | ((bk & FM) << BigFine<CB>::IDX) | (d < 0 ? 0x80000000u : 0u);
       }
     }
   }
@@ -1024,6 +1027,7 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
   constexpr int FB = BigFine<CB>::FB;
   constexpr uint32_t NB = Win<CB>::NB;
   constexpr uint32_t FM = NF - 1;
+  constexpr uint32_t IB = BigFine<CB>::IDX;
   constexpr uint32_t E = 4;  // entries per thread per round: (e, t) order, 1024 per round
   __shared__ uint32_t h[NF], cur[NF], pre[E * 4][NF], lbase[NF], gbase[NF], stage[256 * E];
   __shared__ uint32_t nround;
@@ -1039,9 +1043,9 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = tmp[j + k * 256];
 #pragma unroll
-    for (int k = 0; k < 8; k++) atomicAdd(&h[(v[k] >> BIG_IDX_BITS) & FM], 1u);
+    for (int k = 0; k < 8; k++) atomicAdd(&h[(v[k] >> IB) & FM], 1u);
   }
-  for (; j < b1; j += 256) atomicAdd(&h[(tmp[j] >> BIG_IDX_BITS) & FM], 1u);
+  for (; j < b1; j += 256) atomicAdd(&h[(tmp[j] >> IB) & FM], 1u);
   __syncthreads();
   if (t == 0) {
     uint32_t run = b0, sr = 0;
@@ -1074,7 +1078,7 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
     for (uint32_t e = 0; e < E; e++) {
       const uint32_t j = r0 + e * 256 + t;
       const bool act = j < b1;
-      const uint32_t f = (v[e] >> BIG_IDX_BITS) & FM;
+      const uint32_t f = (v[e] >> IB) & FM;
       // lanes of this wave with the same key: AND of the per-bit ballots
       uint64_t eq = __ballot(act);
 #pragma unroll
@@ -1101,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
       }
       uint32_t x = tot;
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
+      for (int o = 1; o < (int)NF; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if (lane >= (uint32_t)o) x += y;
       }
@@ -1117,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
 #pragma unroll
     for (uint32_t e = 0; e < E; e++) {
       if (rank[e] == ~0u) continue;
-      const uint32_t f = (v[e] >> BIG_IDX_BITS) & FM;
+      const uint32_t f = (v[e] >> IB) & FM;
       stage[lbase[f] + pre[e * 4 + wv][f] + rank[e]] = v[e];
     }
     __syncthreads();
@@ -1125,8 +1129,8 @@ __global__ __launch_bounds__(256) void k_big2_fine(const uint32_t* __restrict__ 
     // positions of each key's run (a wave's stores cover a few lines)
     for (uint32_t q = t; q < nround; q += 256) {
       const uint32_t w = stage[q];
-      const uint32_t f = (w >> BIG_IDX_BITS) & FM;
-      entries[gbase[f] + (q - lbase[f])] = w & (0x80000000u | ((1u << BIG_IDX_BITS) - 1u));
+      const uint32_t f = (w >> IB) & FM;
+      entries[gbase[f] + (q - lbase[f])] = w & (0x80000000u | ((1u << IB) - 1u));
     }
     __syncthreads();  // pre, stage and the bases are rewritten by the next round
   }
@@ -1255,9 +1259,13 @@ static size_t big_min_points() {
 // carry into a near-empty extra window).  Measured at 131 073 points,
 // uniform scalars: c = 13 / 14 / 15 / 16 -> 0.79 / 1.19 / 0.65-0.68 /
 // 0.76-0.83 ms (profiles/r06_shard8_window_ab.jsonl).  KZGX_BIG_WINDOW pins it.
+// c = 17 (65 536 buckets, 15 digit windows) is built and pinnable: 6% fewer
+// additions than c = 16 but a bucket reduction twice as wide, measured 2%
+// slower at 2^19 + 1 and 2^20 + 1 points (profiles/r06_big_window17_ab.jsonl),
+// so never chosen automatically.
 static int big_window_bits(size_t n, int curve) {
   static const int pin = std::getenv("KZGX_BIG_WINDOW") ? std::atoi(std::getenv("KZGX_BIG_WINDOW")) : 0;
-  if (pin >= 12 && pin <= 16) return pin;
+  if (pin >= 12 && pin <= 17) return pin;
   if (curve != KZGX_CURVE_BN254) return 16;
   return n >= ((size_t)1 << 18) ? 16 : 15;
 }
@@ -1512,7 +1520,7 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
   uint32_t K = ctx->seg_k;
   while (K > 8 && emax / K < 131072) K >>= 1;
   static const bool one_pass = std::getenv("KZGX_BIG_ONEPASS") != nullptr;  // A/B: the one-pass sort + merge
-  if (!one_pass && (size_t)W * ctx->n_srs < ((size_t)1 << BIG_IDX_BITS) && n <= (size_t)65535 * 1536) {
+  if (!one_pass && (size_t)W * ctx->n_srs < ((size_t)1 << BigFine<CB>::IDX) && n <= (size_t)65535 * 1536) {
     const uint32_t per2 = big2_per<CB>();
     const size_t nblk2 = (n + per2 - 1) / per2;
     const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
@@ -1601,6 +1609,12 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     KZGX_TRY_HIP(hipGetLastError());
     return big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st, xyzz_out);
   }
+  // the one-pass sort's per-block LDS histograms hold NB counters: not at
+  // c = 17 (256 KB); big_window_bits picks 17 only where the two-pass sort
+  // above applies
+  if constexpr (CB > 16) {
+    return KZGX_ERR_INTERNAL;
+  } else {
   const size_t smax = (emax + K - 1) / K;
   const size_t nwg = (smax + ACC_WG - 1) / ACC_WG;
   const size_t XB = xyzz_words<C>() * sizeof(uint32_t);
@@ -1652,6 +1666,7 @@ static int msm_big_impl(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t*
     KZGX_TRY(big_reduce(ctx->curve, ws.offsets, NB, ws.bsum, ws.rt, d_out, d_out_inf, st, xyzz_out));
   }
   return KZGX_OK;
+  }
 }
 
 template <class C>
@@ -1663,6 +1678,7 @@ static int msm_big(Ctx* ctx, const uint32_t* d_scalars, size_t n, uint32_t* d_ou
     case 14: return msm_big_impl<C, 14>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
     case 15: return msm_big_impl<C, 15>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
     case 16: return msm_big_impl<C, 16>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
+    case 17: return msm_big_impl<C, 17>(ctx, d_scalars, n, d_out, d_out_inf, st, xyzz_out);
     default: return KZGX_ERR_INTERNAL;
   }
 }
