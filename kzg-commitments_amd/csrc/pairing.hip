@@ -335,14 +335,18 @@ __global__ __launch_bounds__(64) void k_g2_terms_w(const uint32_t* __restrict__ 
   terms[t] = acc;
 }
 
-// out[t] = sum of in[8 t .. 8 t + 7] (bounded by count)
-template <class C>
-__global__ __launch_bounds__(64) void k_g2_fold8(const G2J<C>* __restrict__ in, uint32_t count,
-                                                 G2J<C>* __restrict__ out) {
+// out[t] = sum of in[F t .. F t + F - 1] (bounded by count).  F = 2: a G2
+// addition on a lone lane is ~35 us, so the fold runs as a tree of 2:1
+// levels (depth log2 of the term count) -- round 5's 8:1 passes chained 7
+// additions per pass (~260 us each; a 128-point multi-proof verify spent
+// 1.56 ms in polyeval_G2, round 6 trace)
+template <class C, uint32_t F>
+__global__ __launch_bounds__(64) void k_g2_fold(const G2J<C>* __restrict__ in, uint32_t count,
+                                                G2J<C>* __restrict__ out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t * 8 >= count) return;
-  G2J<C> acc = in[t * 8];
-  for (uint32_t k = t * 8 + 1; k < count && k < t * 8 + 8; k++) acc = g2_add<C>(acc, in[k]);
+  if (t * F >= count) return;
+  G2J<C> acc = in[t * F];
+  for (uint32_t k = t * F + 1; k < count && k < t * F + F; k++) acc = g2_add<C>(acc, in[k]);
   out[t] = acc;
 }
 
@@ -354,7 +358,9 @@ __global__ __launch_bounds__(64) void k_g2_sum_tree(const G2J<C>* __restrict__ i
   const uint32_t t = threadIdx.x;
   part[t] = t < count ? in[t] : g2_inf<C>();
   __syncthreads();
-  for (uint32_t s = 32; s >= 1; s >>= 1) {
+  uint32_t s0 = 32;
+  while (s0 > 1 && s0 >= count) s0 >>= 1;  // levels above the count hold only the identity
+  for (uint32_t s = s0; s >= 1; s >>= 1) {
     if (t < s) part[t] = g2_add<C>(part[t], part[t + s]);
     __syncthreads();
   }
@@ -482,7 +488,7 @@ template <class C>
 static int msm_g2_windowed(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, const uint32_t* d_tab,
                            size_t n, uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st) {
   const size_t m = n * G2_TAB_W;
-  const size_t tb = (m + m / 8 + 64) * sizeof(G2J<C>);
+  const size_t tb = (m + (m + 1) / 2 + 64) * sizeof(G2J<C>);  // terms, then the 2:1 ping-pong half
   KZGX_TRY(dev_alloc(ctx, &ctx->d_g2_ws, tb, &ctx->g2_ws_b));
   G2J<C>* a = (G2J<C>*)ctx->d_g2_ws;
   G2J<C>* b = a + m;
@@ -492,9 +498,9 @@ static int msm_g2_windowed(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* 
                        (const G2A<C>*)d_tab, (uint32_t)n, a);
   }
   size_t cnt = m;
-  while (cnt > 64) {
-    const size_t nxt = (cnt + 7) / 8;
-    hipLaunchKernelGGL(k_g2_fold8<C>, dim3((unsigned)((nxt + 63) / 64)), dim3(64), 0, st, a, (uint32_t)cnt, b);
+  while (cnt > 8) {
+    const size_t nxt = (cnt + 1) / 2;
+    hipLaunchKernelGGL((k_g2_fold<C, 2>), dim3((unsigned)((nxt + 63) / 64)), dim3(64), 0, st, a, (uint32_t)cnt, b);
     std::swap(a, b);
     cnt = nxt;
   }
@@ -539,7 +545,7 @@ static int msm_g2_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_sr
 int g2_ws_reserve(Ctx* ctx, size_t n) {
   const size_t m = n * G2_TAB_W;
   const size_t gj = ctx->curve == KZGX_CURVE_BN254 ? sizeof(G2J<BN254G1>) : sizeof(G2J<BLS12381G1>);
-  return dev_alloc(ctx, &ctx->d_g2_ws, (m + m / 8 + 64) * gj, &ctx->g2_ws_b);
+  return dev_alloc(ctx, &ctx->d_g2_ws, (m + (m + 1) / 2 + 64) * gj, &ctx->g2_ws_b);
 }
 
 int msm_g2(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_srs2, size_t n, uint32_t* d_out,

@@ -365,7 +365,8 @@ __global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restri
   p = wave_prod<FR>(p);
   if (lane == 0) {
     if (fe_is_zero<FR>(p)) atomicOr(err, 1u);
-    fe_store<FR>(a + (size_t)i * N, fe_mul<FR>(fe_load<FR>(ym + (size_t)i * N), fe_inv<FR>(p)));
+    // the nodes are public (opening points): the variable-time GCD inverse
+    fe_store<FR>(a + (size_t)i * N, fe_mul<FR>(fe_load<FR>(ym + (size_t)i * N), fe_inv_vt<FR>(p)));
   }
 }
 
