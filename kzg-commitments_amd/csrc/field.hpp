@@ -192,107 +192,6 @@ __device__ __noinline__ Fe<FP> fe_inv(const Fe<FP>& a) {
   return acc;
 }
 
-// a^-1 of a Montgomery value (inv(0) = 0) by the binary extended GCD with
-// Montgomery halvings -- VARIABLE TIME, for public values only (the
-// interpolation weights of the opening points, poly.hip k_interp_weights).
-// u, v from (A, m) with A = a R the stored value, x1 A = u 2^k1, x2 A = v 2^k2
-// (mod m) kept by dividing x by 2^z mod m with one q m addition (q = x -m^-1
-// mod 2^z, z <= 31) each time u or v drops z trailing zeros; at u = 1,
-// x1 = A^-1 2^-0 -- the halvings are exact divisions mod m, so x1 = A^-1.
-// a^-1 R = A^-1 R^2: two products by R^2.  ~360 steps of ~8N instructions
-// in one lane, against the Fermat chain's 256 squarings + 64 products
-// (k_interp_weights at 128 points: 1.65 ms in round 5).
-template <class FP>
-__device__ __noinline__ Fe<FP> fe_inv_vt(const Fe<FP>& a) {
-  uint32_t u[FP::N], v[FP::N], x1[FP::N], x2[FP::N];
-  bool zero = true;
-#pragma unroll
-  for (int i = 0; i < FP::N; i++) {
-    u[i] = a.v[i];
-    v[i] = FP::P[i];
-    x1[i] = i == 0 ? 1u : 0u;
-    x2[i] = 0u;
-    zero = zero && a.v[i] == 0;
-  }
-  if (zero) return fe_zero<FP>();
-  // x <- x / 2^z mod m (x < m, z in [1, 31]): x + q m is divisible by 2^z
-  // with q = x0 (-m^-1) mod 2^z; x + q m < m (1 + 2^z) < 2^(32N), so the
-  // shifted sum is < m + m 2^-z... < 2m: one conditional subtraction
-  auto halve = [](uint32_t (&x)[FP::N], int z) {
-    const uint32_t q = (x[0] * FP::INV) & ((1u << z) - 1u);
-    uint32_t c = 0;
-    uint32_t t[FP::N];
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) {
-      const uint64_t s = (uint64_t)q * FP::P[i] + x[i] + c;
-      t[i] = (uint32_t)s;
-      c = (uint32_t)(s >> 32);
-    }
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) x[i] = __builtin_amdgcn_alignbit(i + 1 < FP::N ? t[i + 1] : c, t[i], z);
-    uint32_t br = 0, d[FP::N];
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) d[i] = __builtin_subc(x[i], FP::P[i], br, &br);
-    if (!br) {
-#pragma unroll
-      for (int i = 0; i < FP::N; i++) x[i] = d[i];
-    }
-  };
-  auto shr = [](uint32_t (&x)[FP::N], int z) {
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) x[i] = __builtin_amdgcn_alignbit(i + 1 < FP::N ? x[i + 1] : 0u, x[i], z);
-  };
-  auto is_one = [](const uint32_t (&x)[FP::N]) {
-    bool one = x[0] == 1u;
-#pragma unroll
-    for (int i = 1; i < FP::N; i++) one = one && x[i] == 0u;
-    return one;
-  };
-  // u -= v, x1 = x1 - x2 mod m
-  auto step = [](uint32_t (&u_)[FP::N], const uint32_t (&v_)[FP::N], uint32_t (&xa)[FP::N], const uint32_t (&xb)[FP::N]) {
-    uint32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) u_[i] = __builtin_subc(u_[i], v_[i], br, &br);
-    br = 0;
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) xa[i] = __builtin_subc(xa[i], xb[i], br, &br);
-    if (br) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int i = 0; i < FP::N; i++) xa[i] = __builtin_addc(xa[i], FP::P[i], c, &c);
-    }
-  };
-  auto tz = [](const uint32_t (&x)[FP::N]) -> int {  // trailing zeros, capped at 31
-    return x[0] ? (int)__builtin_ctz(x[0]) : 31;
-  };
-  // at most 2 * 32 FP::N halvings and as many subtractions
-#pragma unroll 1
-  for (int it = 0; it < 64 * FP::N; it++) {
-    int z;
-    while ((z = tz(u)) > 0) {
-      shr(u, z);
-      halve(x1, z);
-    }
-    while ((z = tz(v)) > 0) {
-      shr(v, z);
-      halve(x2, z);
-    }
-    if (is_one(u) || is_one(v)) break;
-    // u >= v ?
-    uint32_t br = 0, d;
-#pragma unroll
-    for (int i = 0; i < FP::N; i++) d = __builtin_subc(u[i], v[i], br, &br);
-    (void)d;
-    if (!br) step(u, v, x1, x2);
-    else step(v, u, x2, x1);
-  }
-  Fe<FP> r;
-#pragma unroll
-  for (int i = 0; i < FP::N; i++) r.v[i] = is_one(u) ? x1[i] : x2[i];
-  const Fe<FP> r2 = fe_const<FP>(FP::R2);
-  return fe_mul<FP>(fe_mul<FP>(r, r2), r2);
-}
-
 // loads / stores of N-limb elements from 32-bit arrays
 template <class FP>
 KZGX_DEV Fe<FP> fe_load(const uint32_t* p) {

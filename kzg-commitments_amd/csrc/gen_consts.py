@@ -282,6 +282,10 @@ def main():
         field("BLS12381Fr", BLS_R, 8),
         field29("BN254Fp29", BN_P, 9),
         field29("BLS12381Fp29", BLS_P, 14),
+        # the scalar fields in radix 2^29: their inversion by f29_inv_uniform
+        # (poly.hip fe_inv_wave, the interpolation weights)
+        field29("BN254Fr29", BN_R, 9),
+        field29("BLS12381Fr29", BLS_R, 9),
         "struct BN254G1 {",
         "  using Fp = BN254Fp;",
         "  using Fp29 = BN254Fp29;",

@@ -26,6 +26,7 @@
 #include <utility>
 
 #include "field.hpp"
+#include "field29.hpp"
 #include "kzgx_internal.hpp"
 #include "kzgx_setup.hpp"
 
@@ -60,6 +61,42 @@ KZGX_DEV Fe<FR> wave_sum(Fe<FR> a) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) a = fe_add<FR>(a, fe_shfl_xor<FR>(a, m));
   return a;
+}
+
+// the scalar field's radix-2^29 twin (gen_consts.py)
+template <class FR>
+struct Fr29Of;
+template <>
+struct Fr29Of<BN254Fr> {
+  using T = BN254Fr29;
+};
+template <>
+struct Fr29Of<BLS12381Fr> {
+  using T = BLS12381Fr29;
+};
+
+// a^-1 (inv(0) = 0) of lane 0's Montgomery value for the whole wave (every
+// lane calls): the canonical value in radix 2^29 and Montgomery-29 form,
+// Pornin's binary GCD with the bit-serial loop on the scalar ALU and the
+// four linear combinations on four lanes (field29.hpp f29_inv_uniform_raw,
+// ~30 us), back to a 32-bit-limb Montgomery value.  Variable time: public
+// values only (the interpolation nodes).
+template <class FR>
+KZGX_DEV Fe<FR> fe_inv_wave(const Fe<FR>& a) {
+  using F = typename Fr29Of<FR>::T;
+  constexpr int N = FR::N;
+  const Fe<FR> c = fe_from_mont<FR>(a);
+  uint32_t w[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) w[k] = __builtin_amdgcn_readfirstlane(c.v[k]);
+  const F29<F> x = f29_mul<F>(f29_from_words<F, N>(w), f29_const<F>(F::R2));  // c R29
+  const F29<F> i = f29_inv_uniform_raw<F, N>(x, FR::P);                      // c^-1, plain
+  uint32_t o[N];
+  f29_to_words<F, N>(f29_reduce<F>(i), o);
+  Fe<FR> r;
+#pragma unroll
+  for (int k = 0; k < N; k++) r.v[k] = o[k];
+  return fe_to_mont<FR>(r);
 }
 
 template <class FR>
@@ -362,11 +399,13 @@ __global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restri
   Fe<FR> p = fe_one<FR>();
   for (uint32_t j = lane; j < n; j += 64)
     if (j != i) p = fe_mul<FR>(p, fe_sub<FR>(xi, fe_load<FR>(xm + (size_t)j * N)));
-  p = wave_prod<FR>(p);
+  p = wave_prod<FR>(p);  // in every lane (xor butterfly)
+  // the nodes are public (opening points): the variable-time inverse, by the
+  // whole wave (round 5: a Fermat chain in lane 0, 1.65 ms at 128 points)
+  const Fe<FR> pi = fe_inv_wave<FR>(p);
   if (lane == 0) {
     if (fe_is_zero<FR>(p)) atomicOr(err, 1u);
-    // the nodes are public (opening points): the variable-time GCD inverse
-    fe_store<FR>(a + (size_t)i * N, fe_mul<FR>(fe_load<FR>(ym + (size_t)i * N), fe_inv_vt<FR>(p)));
+    fe_store<FR>(a + (size_t)i * N, fe_mul<FR>(fe_load<FR>(ym + (size_t)i * N), pi));
   }
 }
 
