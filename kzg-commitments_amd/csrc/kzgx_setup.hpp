@@ -71,8 +71,14 @@ int vtab_prepare(int curve, const uint32_t* d_g1_0, const uint32_t* g1_comb, uin
 int g1_fold_packed(int curve, const uint32_t* d_rec, size_t count, uint32_t* d_out, hipStream_t st);
 // polyeval_G2's windowed table (pairing.hip k_g2_terms_w) of a generated G2
 // SRS [tau^(start+i)]G2, i < n: G2_TAB_WINDOWS entries per point from the
-// generator's comb (setup.hip k_g2_tab_comb)
-constexpr int G2_TAB_WINDOWS = 16;
+// generator's comb (setup.hip k_g2_tab_comb): entry (i, w) = 2^(G2_TAB_BITS w)
+// [tau^(start+i)]G2
+#ifndef KZGX_G2_TAB_BITS
+#define KZGX_G2_TAB_BITS 8
+#endif
+constexpr int G2_TAB_BITS = KZGX_G2_TAB_BITS;
+static_assert(G2_TAB_BITS == 4 || G2_TAB_BITS == 8 || G2_TAB_BITS == 16, "digits must tile a 32-bit word");
+constexpr int G2_TAB_WINDOWS = 256 / G2_TAB_BITS;
 int g2_table_comb(int curve, const uint32_t* d_tau, size_t start, size_t n, const uint32_t* g2_comb, uint32_t* d_tab,
                   hipStream_t st);
 // the same over projective partial records (one XYZZ point, xyzz_record_words

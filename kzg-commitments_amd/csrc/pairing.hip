@@ -290,13 +290,14 @@ __global__ __launch_bounds__(64) void k_g2_sum(const G2J<C>* __restrict__ terms,
   *out_inf = fin ? 0u : 1u;
 }
 
-// Windowed G2 MSM: tab[i][w] = 2^(16 w) G2[i] (affine Montgomery, zeros for
-// an infinite SRS point), so term i = sum_w d_(i,w) tab[i][w] with 16-bit
-// digits: one thread per (term, window) runs at most 16 doublings and 16
-// additions instead of a 256-bit double-and-add, and the n 16 partial
-// points are folded 8:1 per pass, then by a one-workgroup tree.
-constexpr int G2_TAB_W = 16;
-static_assert(G2_TAB_W == G2_TAB_WINDOWS, "setup.hip k_g2_tab_comb builds the same table");
+// Windowed G2 MSM: tab[i][w] = 2^(B w) G2[i] (affine Montgomery, zeros for
+// an infinite SRS point), so term i = sum_w d_(i,w) tab[i][w] with B-bit
+// digits (B = G2_TAB_BITS): one thread per (term, window) runs at most B
+// doublings and B additions instead of a 256-bit double-and-add, and the
+// n 256/B partial points are folded 2:1 per pass, then by a one-workgroup
+// tree.  Every lone-lane G2 operation is ~27 us, so B = 8 (a chain of ~12
+// operations, one more fold level) beats round 5's B = 16 (~24) by ~0.3 ms.
+constexpr int G2_TAB_W = G2_TAB_WINDOWS;
 
 template <class C>
 __global__ __launch_bounds__(64) void k_g2_tab(const uint32_t* __restrict__ srs2, uint32_t n,
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(64) void k_g2_tab(const uint32_t* __restrict__ srs2
     if (!fin || !g2_to_affine<C>(b, a)) a.x = a.y = f2_zero<C>();
     tab[(size_t)i * G2_TAB_W + w] = a;
     if (w + 1 < G2_TAB_W)
-      for (int k = 0; k < 16; k++) b = g2_dbl<C>(b);
+      for (int k = 0; k < G2_TAB_BITS; k++) b = g2_dbl<C>(b);
   }
 }
 
@@ -322,7 +323,8 @@ __global__ __launch_bounds__(64) void k_g2_terms_w(const uint32_t* __restrict__ 
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * G2_TAB_W) return;
   const uint32_t i = t / G2_TAB_W, w = t % G2_TAB_W;
-  const uint32_t d = (scalars[(size_t)i * 8 + (w >> 1)] >> (16 * (w & 1))) & 0xffffu;
+  const uint32_t d =
+      (scalars[(size_t)i * 8 + ((G2_TAB_BITS * w) >> 5)] >> ((G2_TAB_BITS * w) & 31)) & ((1u << G2_TAB_BITS) - 1u);
   G2A<C> q;
   G2J<C> acc = g2_inf<C>();
   if (d != 0 && g2_from_canon<C>(srs2 + (size_t)i * 4 * C::Fp::N, q)) {

@@ -207,8 +207,8 @@ __global__ __launch_bounds__(64) void k_g2_tab_comb(const uint32_t* __restrict__
   G2J<C> p = g2_inf<C>();
   if (live) {
     Fe<FR> k = fe_zero<FR>();
-    k.v[(16 * w) >> 5] = 1u << ((16 * w) & 31);  // 2^(16 w) < r
-    // tau^(start+i) 2^(16 w) mod r: a Montgomery product with 2^(16 w) R
+    k.v[(G2_TAB_BITS * w) >> 5] = 1u << ((G2_TAB_BITS * w) & 31);  // 2^(B w) < r
+    // tau^(start+i) 2^(B w) mod r: a Montgomery product with 2^(B w) R
     const Fe<FR> e = fe_mul<FR>(srs_power<C>(tau_canon, start + i), fe_to_mont<FR>(k));
 #pragma unroll 1
     for (uint32_t b = 0; b < 8; b++) {
