@@ -1253,6 +1253,26 @@ const uint32_t* g2_table(kzgx_ctx* ctx, size_t n, hipStream_t st) {
   return ctx->d_g2tab;
 }
 
+// the wave verify's setup-derived buffer ([y]G table, the line tables of
+// G2[0] and G2[1]), built on first use after a setup
+int vw_ensure(kzgx_ctx* ctx, hipStream_t st) {
+  if (ctx->vw_ready) return KZGX_OK;
+  KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
+  kzgx::GenTables g;
+  KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, st, &g));
+  KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, g.g1_comb, ctx->d_vw, st));
+  KZGX_TRY_HIP(hipStreamSynchronize(st));  // one-time; later calls may come on other streams
+  ctx->vw_ready = true;
+  return KZGX_OK;
+}
+
+// KZGX_PAIR2_SPLIT=1: the multi-point verify's pairing as round 6's two
+// launches (k_vlines_wave, then k_pair2_wave) instead of k_pair2_fused (A/B)
+bool split_pair2() {
+  static const bool on = std::getenv("KZGX_PAIR2_SPLIT") && std::getenv("KZGX_PAIR2_SPLIT")[0] == '1';
+  return on;
+}
+
 }  // namespace
 
 size_t kzgx_srs_g2_size(const kzgx_ctx* ctx) { return ctx ? ctx->n_srs2 : 0; }
@@ -1423,10 +1443,18 @@ int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, 
   // e(proof, p1) == e(p2, G2[0])  <=>  e(proof, p1) e(-p2, G2[0]) == 1 (one wave, one final
   // exponentiation; the booleans of the reference's FP12_equals)
   uint32_t* d_ok = (uint32_t*)(b + o_o);
-  KZGX_TRY(kzgx::pair2_wave(&ctx->c, g1, fl, g2, fl + 2, (uint32_t*)(b + o_ln), d_ok, st));
-  uint32_t v = 0;
-  KZGX_TRY_HIP(hipMemcpyAsync(&v, d_ok, 4, hipMemcpyDeviceToHost, st));
-  KZGX_TRY_HIP(hipStreamSynchronize(st));
+  uint32_t v = 2;
+  if (!split_pair2()) {  // one launch: [Z(tau)]G2's lines overlap the Miller loop
+    KZGX_TRY(vw_ensure(ctx, st));
+    KZGX_TRY(kzgx::pair2_fused(&ctx->c, g1, fl, g2, fl + 2, ctx->d_vw, d_ok, st));
+    KZGX_TRY_HIP(hipMemcpyAsync(&v, d_ok, 4, hipMemcpyDeviceToHost, st));
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+  }
+  if (v == 2) {  // (a degenerate line chain, or KZGX_PAIR2_SPLIT): two launches
+    KZGX_TRY(kzgx::pair2_wave(&ctx->c, g1, fl, g2, fl + 2, (uint32_t*)(b + o_ln), d_ok, st));
+    KZGX_TRY_HIP(hipMemcpyAsync(&v, d_ok, 4, hipMemcpyDeviceToHost, st));
+    KZGX_TRY_HIP(hipStreamSynchronize(st));
+  }
   *ok = v ? 1 : 0;
   return KZGX_OK;
 }
@@ -1440,14 +1468,7 @@ int kzgx_verify_single_batch_device(kzgx_ctx* ctx, const void* d_commits, const 
   if (ctx->c.n_srs == 0 || ctx->n_srs2 < 2) return KZGX_ERR_NO_SRS;
   hipStream_t st = pick(ctx, stream);
   if (count <= ctx->vw_max) {
-    if (!ctx->vw_ready) {
-      KZGX_TRY(kzgx::dev_alloc(&ctx->c, (void**)&ctx->d_vw, kzgx::verify_wave_bytes(ctx->c.curve), &ctx->vw_b));
-      kzgx::GenTables g;
-      KZGX_TRY(kzgx::gen_tables_get(ctx->c.curve, ctx->c.device, st, &g));
-      KZGX_TRY(kzgx::verify_wave_prepare(&ctx->c, ctx->d_srs_canon, ctx->d_srs2_canon, g.g1_comb, ctx->d_vw, st));
-      KZGX_TRY_HIP(hipStreamSynchronize(st));  // one-time; later calls may come on other streams
-      ctx->vw_ready = true;
-    }
+    KZGX_TRY(vw_ensure(ctx, st));
     return kzgx::verify_wave_batch(&ctx->c, (const uint32_t*)d_commits, (const uint32_t*)d_commit_inf,
                                    (const uint32_t*)d_proofs, (const uint32_t*)d_proof_inf, (const uint32_t*)d_z,
                                    (const uint32_t*)d_y, count, ctx->d_srs_canon, ctx->d_vw, (uint32_t*)d_ok, st);

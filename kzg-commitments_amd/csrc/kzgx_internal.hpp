@@ -338,6 +338,11 @@ int verify_wave_batch(Ctx* ctx, const uint32_t* d_commits, const uint32_t* d_com
 size_t pair2_wave_scratch_bytes(int curve);
 int pair2_wave(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
                uint32_t* d_scratch, uint32_t* d_ok, hipStream_t st);
+// the same with Q_1 = G2[0] (d_vw: verify_wave_prepare's buffer) in one
+// launch of three waves, Q_0's line chain overlapping the Miller loop; *ok = 2
+// for a degenerate chain (rerun pair2_wave); d_q: Q_0 alone, d_q_inf: its flag
+int pair2_fused(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+                const uint32_t* d_vw, uint32_t* d_ok, hipStream_t st);
 int g1_sub(Ctx* ctx, const uint32_t* d_a, const uint32_t* d_a_inf, const uint32_t* d_b, const uint32_t* d_b_inf,
            uint32_t* d_out, uint32_t* d_out_inf, hipStream_t st);
 

@@ -394,7 +394,7 @@ KZGX_DEV void vw_mul(uint32_t dst_o, uint32_t a_o, uint32_t b_o, uint32_t prod_o
 // 18 Fp2 products f_i l_t as 54 Fp (Karatsuba) parts, one per lane, then
 // lane (k, im) < 12 folds the three products landing on w^k (xi for the
 // wrapped ones) lazily
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o, int lane) {
   using F = typename C::Fp29;
   using V = VWave<C>;
@@ -405,7 +405,7 @@ KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o, int la
     const int i = lane / 9, t = (lane / 3) % 3;
     vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(f + i * E2), vw_ld2<C>(line + t * E2), lane % 3));
   }
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 12) {
     // (three terms: a two-lane split measured slower, 2.29 vs 1.98 us)
     const int k = lane >> 1, im = lane & 1;
@@ -421,7 +421,7 @@ KZGX_DEV void vw_mul_line(uint32_t f_o, uint32_t line_o, uint32_t prod_o, int la
     }
     vw_st<C>(f + k * E2 + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // dst = a^2 for any a: the 21 products a_i a_j (i <= j) as 63 Fp
@@ -431,7 +431,7 @@ template <class C>
 KZGX_DEV int vw_pair_index(int i, int j) {
   return i * 6 - (i * (i - 1)) / 2 + (j - i);
 }
-template <class C>
+template <class C, bool WS = false>
 KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o, int lane) {
   using F = typename C::Fp29;
   constexpr int E2 = VWave<C>::E2, L = VWave<C>::L, PL = VWave<C>::PL;
@@ -445,7 +445,7 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o, int lane) {
     }
     vw_stp<C>(prod + lane * PL, vw_part<C>(vw_ld2<C>(a + i * E2), vw_ld2<C>(a + (i + idx) * E2), lane % 3));
   }
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 24) {
     // c_k = sum_i a_i a_{(k - i) mod 6} (xi for the wrapped ones): one
     // uniform pass over i, reading the unordered pair's parts -- a cross
@@ -466,7 +466,7 @@ KZGX_DEV void vw_sqr(uint32_t dst_o, uint32_t a_o, uint32_t prod_o, int lane) {
     lin_pair_sum<F>(acc);
     if (!h) vw_st<C>(dst + k * E2 + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // Granger-Scott squaring of a cyclotomic element (f12_cyclo_sqr) with one Fp
@@ -598,7 +598,9 @@ template <class C, bool WS = false>
 KZGX_DEV void vw_copy(uint32_t dst_o, uint32_t a_o) {
   uint32_t* dst = vw_smem + dst_o;
   const uint32_t* a = vw_smem + a_o;
-  for (int w = vw_lane<WS>(); w < VWave<C>::E12; w += WS ? 64 : (int)blockDim.x) dst[w] = a[w];
+  // (at most two waves copy: k_pair2_fused's third wave has left by then)
+  const int step = WS ? 64 : ((int)blockDim.x < 128 ? (int)blockDim.x : 128);
+  for (int w = vw_lane<WS>(); w < VWave<C>::E12; w += step) dst[w] = a[w];
   vw_sync<WS>();
 }
 
@@ -940,6 +942,62 @@ KZGX_TW void vw_miller(uint32_t f, int use_mask, uint32_t prod) {
   vw_mul<C>(f, f, f + V::E12, prod);
 }
 
+// vw_miller with per-wave syncs only (k_pair2_fused): wave q runs pairing
+// q's loop on its own slots and product parts, so neither waits at the
+// other's barriers; with `wait`, wave 0 takes line s only once the LDS word
+// at ready_o (the producer wave's count of published lines) exceeds s
+// (ready_o + 1 set: it gave up waiting).  Then
+// the workgroup barrier and f = f_0 f_1.
+template <class C>
+KZGX_TW void vw_miller_ws(uint32_t f, int use_mask, uint32_t prod, uint32_t ready_o, bool wait) {
+  using P = typename PairOf<C>::T;
+  using V = VWave<C>;
+  constexpr int NLOOP = V::NL - (P::D_TWIST ? 2 : 0);
+  const int q = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
+  const uint32_t fq = f + (uint32_t)q * V::E12;
+  const uint32_t pq = q ? (uint32_t)V::O_PROD2 : prod;
+  const bool w0 = wait && q == 0;
+  volatile const uint32_t* ready = vw_smem + ready_o;
+  int i = P::LOOP_BITS - 2;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < V::NL; s++) {
+    if (s < NLOOP) {
+      if (add_next) {
+        add_next = false;
+        i--;
+      } else {
+        if (i != P::LOOP_BITS - 2) vw_sqr<C, true>(fq, fq, pq, lane);
+        add_next = (P::LOOP[i >> 6] >> (i & 63)) & 1ull;
+        if (!add_next) i--;
+      }
+    } else if (s == NLOOP && P::LOOP_NEG) {
+      vw_conj<C, true>(fq, fq, lane);
+    }
+    if (w0) {
+      // bounded (~0.5 s): a producer that never delivers marks the result
+      // for the two-launch rerun instead of holding the GPU
+      uint32_t spins = 0;
+      while ((uint32_t)__builtin_amdgcn_readfirstlane((int)*ready) <= (uint32_t)s) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == (1u << 22)) {
+          if (lane == 0) vw_smem[ready_o + 1] = 1u;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    vw_mul_line<C, true>(fq, V::O_LINES + (q * V::NL + s) * V::LW, pq, lane);
+  }
+  if (NLOOP == V::NL && P::LOOP_NEG) vw_conj<C, true>(fq, fq, lane);
+  if (!((use_mask >> q) & 1) && lane < 12) {
+    using F = typename C::Fp29;
+    vw_st<C>(vw_smem + fq + lane * V::L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  }
+  __syncthreads();
+  vw_mul<C>(f, f, f + V::E12, prod);
+}
+
 // The same line table for a variable Q with the G2 chain spread over a wave
 // (k_vlines runs it on one lane: ~25 dependent Fp2 operations per step).
 // Each step is a few rounds of independent Fp2 products, one Karatsuba part
@@ -961,69 +1019,69 @@ struct VLine {
   static constexpr int WORDS = FLAG + 4;
 };
 
-template <class C>
+template <class C, int OFF = 0>
 KZGX_DEV uint32_t* vl_slot(int k) {
-  return vw_smem + k * VLine<C>::E2;
+  return vw_smem + OFF + k * VLine<C>::E2;
 }
 // lanes < 3 n: part (lane % 3) of product lane / 3, operands from `ops`
-template <class C, class Ops>
+template <class C, int OFF, bool WS, class Ops>
 KZGX_DEV void vl_parts(int n, Ops ops) {
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   if (lane < 3 * n) {
     Fp2<C> x, y;
     ops(lane / 3, x, y);
-    vw_st<C>(vw_smem + VLine<C>::PROD + lane * VLine<C>::L, vw_part<C>(x, y, lane % 3));
+    vw_st<C>(vw_smem + OFF + VLine<C>::PROD + lane * VLine<C>::L, vw_part<C>(x, y, lane % 3));
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
-template <class C>
+template <class C, int OFF = 0>
 KZGX_DEV const uint32_t* vl_prod(int k) {
-  return vw_smem + VLine<C>::PROD + 3 * k * VLine<C>::L;
+  return vw_smem + OFF + VLine<C>::PROD + 3 * k * VLine<C>::L;
 }
-template <class C>
+template <class C, int OFF = 0>
 KZGX_DEV const uint32_t* vl_comp(int slot, int im) {
-  return vw_smem + slot * VLine<C>::E2 + im * VLine<C>::L;
+  return vw_smem + OFF + slot * VLine<C>::E2 + im * VLine<C>::L;
 }
 
-template <class C>
+template <class C, int OFF = 0, bool WS = false>
 KZGX_DEV void vl_dbl_wave(uint32_t* out) {
   using F = typename C::Fp29;
   using S = VLine<C>;
   constexpr int L = S::L, E2 = S::E2;
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   // round 1: A = X^2, B = Y^2, ZZ = Z^2, YZ = Y Z
-  vl_parts<C>(4, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+  vl_parts<C, OFF, WS>(4, [&](int k, Fp2<C>& x, Fp2<C>& y) {
     const int a = k == 0 ? S::X : k == 1 ? S::Y : k == 2 ? S::Z : S::Y;
     const int b = k == 3 ? S::Z : a;
-    x = vw_ld2<C>(vl_slot<C>(a));
-    y = vw_ld2<C>(vl_slot<C>(b));
+    x = vw_ld2<C>(vl_slot<C, OFF>(a));
+    y = vw_ld2<C>(vl_slot<C, OFF>(b));
   });
   if (lane < 8) {
     const int k = lane >> 1, im = lane & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add_f2<F>(acc, vl_prod<C>(k), im, false, 1);
+    lin_add_f2<F>(acc, vl_prod<C, OFF>(k), im, false, 1);
     const int dst = k == 0 ? S::A : k == 1 ? S::B : k == 2 ? S::ZZ : S::YZ;
-    vw_st<C>(vl_slot<C>(dst) + im * L, lin_fin<F>(acc));
+    vw_st<C>(vl_slot<C, OFF>(dst) + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
+  vw_sync<WS>();
   // round 2: 2YZ ZZ, E ZZ, E X, B^2, (X + B)^2, E^2 with E = 3A
-  vl_parts<C>(6, [&](int k, Fp2<C>& x, Fp2<C>& y) {
-    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+  vl_parts<C, OFF, WS>(6, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C, OFF>(S::A));
     const Fp2<C> E = f2_add<C>(f2_dbl<C>(a), a);
     if (k == 0) {
-      x = f2_dbl<C>(vw_ld2<C>(vl_slot<C>(S::YZ)));
-      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+      x = f2_dbl<C>(vw_ld2<C>(vl_slot<C, OFF>(S::YZ)));
+      y = vw_ld2<C>(vl_slot<C, OFF>(S::ZZ));
     } else if (k == 1) {
       x = E;
-      y = vw_ld2<C>(vl_slot<C>(S::ZZ));
+      y = vw_ld2<C>(vl_slot<C, OFF>(S::ZZ));
     } else if (k == 2) {
       x = E;
-      y = vw_ld2<C>(vl_slot<C>(S::X));
+      y = vw_ld2<C>(vl_slot<C, OFF>(S::X));
     } else if (k == 3) {
-      x = y = vw_ld2<C>(vl_slot<C>(S::B));
+      x = y = vw_ld2<C>(vl_slot<C, OFF>(S::B));
     } else if (k == 4) {
-      x = y = f2_add<C>(vw_ld2<C>(vl_slot<C>(S::X)), vw_ld2<C>(vl_slot<C>(S::B)));
+      x = y = f2_add<C>(vw_ld2<C>(vl_slot<C, OFF>(S::X)), vw_ld2<C>(vl_slot<C, OFF>(S::B)));
     } else {
       x = y = E;
     }
@@ -1035,107 +1093,107 @@ KZGX_DEV void vl_dbl_wave(uint32_t* out) {
     LinAcc<F> acc;
     lin_init<F>(acc);
     switch (w) {
-      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
-      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -1); break;
+      case 0: lin_add_f2<F>(acc, vl_prod<C, OFF>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C, OFF>(1), im, false, -1); break;
       case 2:
-        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
-        lin_add<F>(acc, vl_comp<C>(S::B, im), -2);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(2), im, false, 1);
+        lin_add<F>(acc, vl_comp<C, OFF>(S::B, im), -2);
         break;
-      case 3: lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1); break;
+      case 3: lin_add_f2<F>(acc, vl_prod<C, OFF>(3), im, false, 1); break;
       case 4:
-        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, 2);
-        lin_add<F>(acc, vl_comp<C>(S::A, im), -2);
-        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, -2);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(4), im, false, 2);
+        lin_add<F>(acc, vl_comp<C, OFF>(S::A, im), -2);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(3), im, false, -2);
         break;
       case 5:
-        lin_add_f2<F>(acc, vl_prod<C>(5), im, false, 1);
-        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -4);
-        lin_add<F>(acc, vl_comp<C>(S::A, im), 4);
-        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 4);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(5), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(4), im, false, -4);
+        lin_add<F>(acc, vl_comp<C, OFF>(S::A, im), 4);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(3), im, false, 4);
         break;
-      default: lin_add<F>(acc, vl_comp<C>(S::YZ, im), 2); break;
+      default: lin_add<F>(acc, vl_comp<C, OFF>(S::YZ, im), 2); break;
     }
     const F29<F> v = lin_fin<F>(acc);
     if (w < 3) {
       vw_st<C>(out + w * E2 + im * L, v);
     } else {
       const int dst = w == 3 ? S::CC : w == 4 ? S::D : w == 5 ? S::X : S::Z;
-      vw_st<C>(vl_slot<C>(dst) + im * L, v);
+      vw_st<C>(vl_slot<C, OFF>(dst) + im * L, v);
     }
   }
-  __syncthreads();
+  vw_sync<WS>();
   // round 3: Y3 = E (D - X3) - 8 C
-  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) {
-    const Fp2<C> a = vw_ld2<C>(vl_slot<C>(S::A));
+  vl_parts<C, OFF, WS>(1, [&](int, Fp2<C>& x, Fp2<C>& y) {
+    const Fp2<C> a = vw_ld2<C>(vl_slot<C, OFF>(S::A));
     x = f2_add<C>(f2_dbl<C>(a), a);
-    y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::D)), vw_ld2<C>(vl_slot<C>(S::X)));
+    y = f2_sub<C>(vw_ld2<C>(vl_slot<C, OFF>(S::D)), vw_ld2<C>(vl_slot<C, OFF>(S::X)));
   });
   if (lane < 2) {
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add_f2<F>(acc, vl_prod<C>(0), lane, false, 1);
-    lin_add<F>(acc, vl_comp<C>(S::CC, lane), -8);
-    vw_st<C>(vl_slot<C>(S::Y) + lane * L, lin_fin<F>(acc));
+    lin_add_f2<F>(acc, vl_prod<C, OFF>(0), lane, false, 1);
+    lin_add<F>(acc, vl_comp<C, OFF>(S::CC, lane), -8);
+    vw_st<C>(vl_slot<C, OFF>(S::Y) + lane * L, lin_fin<F>(acc));
   }
-  __syncthreads();
-  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::Z)))) vw_smem[S::FLAG] = 1u;  // T = O
-  __syncthreads();
+  vw_sync<WS>();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C, OFF>(S::Z)))) vw_smem[OFF + S::FLAG] = 1u;  // T = O
+  vw_sync<WS>();
 }
 
 // T += q (q = slots qx, qy) and the chord line into out
-template <class C>
+template <class C, int OFF = 0, bool WS = false>
 KZGX_DEV void vl_add_wave(int qx, int qy, uint32_t* out) {
   using F = typename C::Fp29;
   using S = VLine<C>;
   constexpr int L = S::L, E2 = S::E2;
-  const int lane = threadIdx.x;
+  const int lane = vw_lane<WS>();
   auto fin1 = [&](int k, int dst, int d) {  // lanes 2k, 2k+1: slot dst = d * product k
     if ((lane >> 1) == k) {
       LinAcc<F> acc;
       lin_init<F>(acc);
-      lin_add_f2<F>(acc, vl_prod<C>(k), lane & 1, false, d);
-      vw_st<C>(vl_slot<C>(dst) + (lane & 1) * L, lin_fin<F>(acc));
+      lin_add_f2<F>(acc, vl_prod<C, OFF>(k), lane & 1, false, d);
+      vw_st<C>(vl_slot<C, OFF>(dst) + (lane & 1) * L, lin_fin<F>(acc));
     }
   };
   // Z1Z1 = Z^2
-  vl_parts<C>(1, [&](int, Fp2<C>& x, Fp2<C>& y) { x = y = vw_ld2<C>(vl_slot<C>(S::Z)); });
+  vl_parts<C, OFF, WS>(1, [&](int, Fp2<C>& x, Fp2<C>& y) { x = y = vw_ld2<C>(vl_slot<C, OFF>(S::Z)); });
   fin1(0, S::Z1Z1, 1);
-  __syncthreads();
+  vw_sync<WS>();
   // U2 = qx Z1Z1, ZZZ = Z Z1Z1
-  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
-    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qx : S::Z));
-    y = vw_ld2<C>(vl_slot<C>(S::Z1Z1));
+  vl_parts<C, OFF, WS>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C, OFF>(k == 0 ? qx : S::Z));
+    y = vw_ld2<C>(vl_slot<C, OFF>(S::Z1Z1));
   });
   fin1(0, S::U2, 1);
   fin1(1, S::ZZZ, 1);
-  __syncthreads();
+  vw_sync<WS>();
   if (lane < 2) {  // H = U2 - X
     const int im = lane;
-    vw_st<C>(vl_slot<C>(S::H) + im * L, fp_sub<F>(vw_ld<C>(vl_comp<C>(S::U2, im)), vw_ld<C>(vl_comp<C>(S::X, im))));
+    vw_st<C>(vl_slot<C, OFF>(S::H) + im * L, fp_sub<F>(vw_ld<C>(vl_comp<C, OFF>(S::U2, im)), vw_ld<C>(vl_comp<C, OFF>(S::X, im))));
   }
-  __syncthreads();
+  vw_sync<WS>();
   // S2 = qy ZZZ, HH = H^2, ZH = Z H
-  vl_parts<C>(3, [&](int k, Fp2<C>& x, Fp2<C>& y) {
-    x = vw_ld2<C>(vl_slot<C>(k == 0 ? qy : k == 1 ? S::H : S::Z));
-    y = vw_ld2<C>(vl_slot<C>(k == 0 ? S::ZZZ : S::H));
+  vl_parts<C, OFF, WS>(3, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+    x = vw_ld2<C>(vl_slot<C, OFF>(k == 0 ? qy : k == 1 ? S::H : S::Z));
+    y = vw_ld2<C>(vl_slot<C, OFF>(k == 0 ? S::ZZZ : S::H));
   });
   // r = 2 (S2 - Y), I = 4 HH, Z3 = 2 ZH
   if (lane < 6) {
     const int w = lane >> 1, im = lane & 1;
     LinAcc<F> acc;
     lin_init<F>(acc);
-    lin_add_f2<F>(acc, vl_prod<C>(w), im, false, w == 1 ? 4 : 2);
-    if (w == 0) lin_add<F>(acc, vl_comp<C>(S::Y, im), -2);
-    vw_st<C>(vl_slot<C>(w == 0 ? S::R : w == 1 ? S::I : S::Z3) + im * L, lin_fin<F>(acc));
+    lin_add_f2<F>(acc, vl_prod<C, OFF>(w), im, false, w == 1 ? 4 : 2);
+    if (w == 0) lin_add<F>(acc, vl_comp<C, OFF>(S::Y, im), -2);
+    vw_st<C>(vl_slot<C, OFF>(w == 0 ? S::R : w == 1 ? S::I : S::Z3) + im * L, lin_fin<F>(acc));
   }
-  __syncthreads();
-  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C>(S::H)))) vw_smem[S::FLAG] = 1u;  // T = +-q
+  vw_sync<WS>();
+  if (lane == 0 && f2_is_zero<C>(vw_ld2<C>(vl_slot<C, OFF>(S::H)))) vw_smem[OFF + S::FLAG] = 1u;  // T = +-q
   // J = H I, V = X I, r^2, r qx, qy Z3
-  vl_parts<C>(5, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+  vl_parts<C, OFF, WS>(5, [&](int k, Fp2<C>& x, Fp2<C>& y) {
     const int a = k == 0 ? S::H : k == 1 ? S::X : k == 4 ? qy : S::R;
     const int b = k <= 1 ? S::I : k == 2 ? S::R : k == 3 ? qx : S::Z3;
-    x = vw_ld2<C>(vl_slot<C>(a));
-    y = vw_ld2<C>(vl_slot<C>(b));
+    x = vw_ld2<C>(vl_slot<C, OFF>(a));
+    y = vw_ld2<C>(vl_slot<C, OFF>(b));
   });
   // J, V; X3 = r^2 - J - 2V; line: w0c = Z3, w1c = -r, w3c = r qx - qy Z3
   if (lane < 12) {
@@ -1143,54 +1201,54 @@ KZGX_DEV void vl_add_wave(int qx, int qy, uint32_t* out) {
     LinAcc<F> acc;
     lin_init<F>(acc);
     switch (w) {
-      case 0: lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1); break;
-      case 1: lin_add_f2<F>(acc, vl_prod<C>(1), im, false, 1); break;
+      case 0: lin_add_f2<F>(acc, vl_prod<C, OFF>(0), im, false, 1); break;
+      case 1: lin_add_f2<F>(acc, vl_prod<C, OFF>(1), im, false, 1); break;
       case 2:
-        lin_add_f2<F>(acc, vl_prod<C>(2), im, false, 1);
-        lin_add_f2<F>(acc, vl_prod<C>(0), im, false, -1);
-        lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(2), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(0), im, false, -1);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(1), im, false, -2);
         break;
-      case 3: lin_add<F>(acc, vl_comp<C>(S::Z3, im), 1); break;
-      case 4: lin_add<F>(acc, vl_comp<C>(S::R, im), -1); break;
+      case 3: lin_add<F>(acc, vl_comp<C, OFF>(S::Z3, im), 1); break;
+      case 4: lin_add<F>(acc, vl_comp<C, OFF>(S::R, im), -1); break;
       default:
-        lin_add_f2<F>(acc, vl_prod<C>(3), im, false, 1);
-        lin_add_f2<F>(acc, vl_prod<C>(4), im, false, -1);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(3), im, false, 1);
+        lin_add_f2<F>(acc, vl_prod<C, OFF>(4), im, false, -1);
         break;
     }
     const F29<F> v = lin_fin<F>(acc);
     if (w < 3)
-      vw_st<C>(vl_slot<C>(w == 0 ? S::J : w == 1 ? S::V : S::D) + im * L, v);  // D holds X3 for now
+      vw_st<C>(vl_slot<C, OFF>(w == 0 ? S::J : w == 1 ? S::V : S::D) + im * L, v);  // D holds X3 for now
     else
       vw_st<C>(out + (w - 3) * E2 + im * L, v);
   }
-  __syncthreads();
+  vw_sync<WS>();
   // Y3 = r (V - X3) - 2 Y J
-  vl_parts<C>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
+  vl_parts<C, OFF, WS>(2, [&](int k, Fp2<C>& x, Fp2<C>& y) {
     if (k == 0) {
-      x = vw_ld2<C>(vl_slot<C>(S::R));
-      y = f2_sub<C>(vw_ld2<C>(vl_slot<C>(S::V)), vw_ld2<C>(vl_slot<C>(S::D)));
+      x = vw_ld2<C>(vl_slot<C, OFF>(S::R));
+      y = f2_sub<C>(vw_ld2<C>(vl_slot<C, OFF>(S::V)), vw_ld2<C>(vl_slot<C, OFF>(S::D)));
     } else {
-      x = vw_ld2<C>(vl_slot<C>(S::Y));
-      y = vw_ld2<C>(vl_slot<C>(S::J));
+      x = vw_ld2<C>(vl_slot<C, OFF>(S::Y));
+      y = vw_ld2<C>(vl_slot<C, OFF>(S::J));
     }
   });
   if (lane < 6) {  // new T: X = X3, Y = Y3, Z = Z3
     const int w = lane >> 1, im = lane & 1;
     F29<F> v;
     if (w == 0) {
-      v = vw_ld<C>(vl_comp<C>(S::D, im));
+      v = vw_ld<C>(vl_comp<C, OFF>(S::D, im));
     } else if (w == 1) {
       LinAcc<F> acc;
       lin_init<F>(acc);
-      lin_add_f2<F>(acc, vl_prod<C>(0), im, false, 1);
-      lin_add_f2<F>(acc, vl_prod<C>(1), im, false, -2);
+      lin_add_f2<F>(acc, vl_prod<C, OFF>(0), im, false, 1);
+      lin_add_f2<F>(acc, vl_prod<C, OFF>(1), im, false, -2);
       v = lin_fin<F>(acc);
     } else {
-      v = vw_ld<C>(vl_comp<C>(S::Z3, im));
+      v = vw_ld<C>(vl_comp<C, OFF>(S::Z3, im));
     }
-    vw_st<C>(vl_slot<C>(w) + im * L, v);  // slots X, Y, Z are 0, 1, 2
+    vw_st<C>(vl_slot<C, OFF>(w) + im * L, v);  // slots X, Y, Z are 0, 1, 2
   }
-  __syncthreads();
+  vw_sync<WS>();
 }
 
 // block q: the line table of Q_q (canonical) into lines + q NL LW
@@ -1465,6 +1523,140 @@ __global__ __launch_bounds__(128) void k_pair2_wave(const uint32_t* __restrict__
   vw_pair_tail<C>(vlines, ok);
 }
 
+// verify_proof with more than one point in one workgroup of three waves:
+// e(P_0, Q_0) e(-P_1, Q_1) == 1 with Q_0 = [Z(tau)]G2 (canonical, variable)
+// and Q_1 = G2[0], whose line table the setup built (verify_wave_prepare,
+// table 0).  Wave 2 runs Q_0's G2 chain (vl_dbl_wave / vl_add_wave with
+// per-wave syncs in its own LDS region), scales each line by P_0's (yP, xP)
+// into wave 0's line slots and publishes it (the LDS word READY counts the
+// lines out); wave 0 squares and multiplies the lines in as they arrive,
+// wave 1 runs Q_1's loop from the table (vw_miller_ws).  So the chain and
+// the Miller loop overlap instead of running as two launches (k_vlines_wave,
+// then k_pair2_wave).  The producer leaves after its last line (a finished
+// wave no longer counts at the workgroup barriers); the two waves then take
+// the final exponentiation as k_pair2_wave.  A degenerate chain (T = O or
+// T = +-Q, impossible for Q of order r) gives *ok = 2: the caller reruns
+// the two-launch path, whose k_vlines_redo recomputes it on one lane.
+template <class C>
+struct Fused {
+  static constexpr int OFF = (VWave<C>::WORDS + 3) & ~3;  // the producer's VLine region
+  static constexpr int READY = OFF + VLine<C>::WORDS;  // lines published; READY + 1: wave 0 gave up waiting
+  static constexpr int WORDS = READY + 2;
+  static_assert(WORDS * 4 <= 160 * 1024, "one workgroup's LDS");
+};
+
+template <class C>
+__global__ __launch_bounds__(192) void k_pair2_fused(const uint32_t* __restrict__ p, const uint32_t* __restrict__ p_inf,
+                                                    const uint32_t* __restrict__ q0,
+                                                    const uint32_t* __restrict__ q0_inf,
+                                                    const uint32_t* __restrict__ tab_lines,
+                                                    const uint32_t* __restrict__ tab_qfin, uint32_t* __restrict__ ok) {
+  using P = typename PairOf<C>::T;
+  using F = typename C::Fp29;
+  using V = VWave<C>;
+  using S = VLine<C>;
+  constexpr int N = C::Fp::N, L = V::L, E2 = V::E2, OFF = Fused<C>::OFF, READY = Fused<C>::READY;
+  uint32_t* scale = vw_smem + V::O_SCALE;
+  uint32_t* flag = vw_smem + V::O_FLAG;
+  uint32_t* lines = vw_smem + V::O_LINES;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 2; q++) {
+      Affine<C> a;
+      const bool fin = affine_from_canonical<C>(p + q * 2 * N, a) && !(p_inf && p_inf[q]);
+      vw_st<C>(scale + (q * 3 + 0) * L, q ? fp_neg<F>(a.y) : a.y);
+      vw_st<C>(scale + (q * 3 + 1) * L, a.x);
+      vw_st<C>(scale + (q * 3 + 2) * L, f29_one<F>());
+      flag[q] = fin ? 1u : 0u;
+    }
+    flag[1] = flag[1] && tab_qfin[0];
+    vw_smem[READY] = 0u;
+    vw_smem[READY + 1] = 0u;
+  }
+  if (threadIdx.x == 128) {
+    G2A<C> Q;
+    const bool fin = g2_from_canon<C>(q0, Q) && !(q0_inf && *q0_inf);
+    vw_smem[OFF + S::FLAG] = fin ? 0u : 2u;
+    vw_st2<C>(vl_slot<C, OFF>(S::X), Q.x);
+    vw_st2<C>(vl_slot<C, OFF>(S::Y), Q.y);
+    vw_st2<C>(vl_slot<C, OFF>(S::Z), f2_one<C>());
+    vw_st2<C>(vl_slot<C, OFF>(S::QX), Q.x);
+    vw_st2<C>(vl_slot<C, OFF>(S::QY), Q.y);
+    if (P::D_TWIST) {
+      const G2A<C> q1 = twist_frob<C>(Q);
+      G2A<C> q2 = twist_frob<C>(q1);
+      q2.y = f2_neg<C>(q2.y);
+      vw_st2<C>(vl_slot<C, OFF>(S::Q1X), q1.x);
+      vw_st2<C>(vl_slot<C, OFF>(S::Q1Y), q1.y);
+      vw_st2<C>(vl_slot<C, OFF>(S::Q2X), q2.x);
+      vw_st2<C>(vl_slot<C, OFF>(S::Q2Y), q2.y);
+    }
+  }
+  __syncthreads();
+  const bool use0 = flag[0] != 0 && vw_smem[OFF + S::FLAG] == 0u, use1 = flag[1] != 0;
+  if (w == 2) {  // the producer: Q_0's lines, scaled, one at a time
+    if (!use0) return;
+    int s = 0;
+    auto publish = [&]() {
+      uint32_t* out = lines + s * V::LW;
+      if (lane < 2) vw_st2<C>(out + lane * E2, f2_mul_fp<C>(vw_ld2<C>(out + lane * E2), vw_ld<C>(scale + lane * L)));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      s++;
+      if (lane == 0) *(volatile uint32_t*)(vw_smem + READY) = (uint32_t)s;
+    };
+#pragma unroll 1
+    for (int i = P::LOOP_BITS - 2; i >= 0; i--) {
+      vl_dbl_wave<C, OFF, true>(lines + s * V::LW);
+      publish();
+      if ((P::LOOP[i >> 6] >> (i & 63)) & 1ull) {
+        vl_add_wave<C, OFF, true>(S::QX, S::QY, lines + s * V::LW);
+        publish();
+      }
+    }
+    if (P::LOOP_NEG && lane < 2) {
+      uint32_t* y = vl_slot<C, OFF>(S::Y) + lane * S::L;
+      vw_st<C>(y, fp_neg<F>(vw_ld<C>(y)));
+    }
+    vw_sync<true>();
+    if (P::D_TWIST) {
+      vl_add_wave<C, OFF, true>(S::Q1X, S::Q1Y, lines + s * V::LW);
+      publish();
+      vl_add_wave<C, OFF, true>(S::Q2X, S::Q2Y, lines + s * V::LW);
+      publish();
+    }
+    return;
+  }
+  // wave 1: Q_1's table lines scaled by -P_1; wave 0 (Q_0 unused): zeros
+  if (w == 1) {
+    for (int t = lane; t < V::NL * 3; t += 64) {
+      const int c = t % 3;
+      vw_st2<C>(lines + (V::NL * 3 + t) * E2,
+                use1 ? f2_mul_fp<C>(vw_ld2<C>(tab_lines + (size_t)t * E2), vw_ld<C>(scale + (3 + c) * L))
+                     : f2_zero<C>());
+    }
+  } else if (!use0) {
+    for (int t = lane; t < V::NL * 3; t += 64) vw_st2<C>(lines + t * E2, f2_zero<C>());
+  }
+  constexpr uint32_t f = V::O_SLOT, pr = V::O_PROD;
+  if (lane < 12) vw_st<C>(vw_smem + f + w * V::E12 + lane * L, lane == 0 ? f29_one<F>() : f29_zero<F>());
+  vw_sync<true>();
+  vw_miller_ws<C>(f, (use0 ? 1 : 0) | (use1 ? 2 : 0), pr, READY, use0);
+  vw_final_exp<C>(V::O_SLOT, pr);
+  if (threadIdx.x < 12) {
+    const F29<F> v = f29_reduce<F>(vw_ld<C>(vw_smem + f + threadIdx.x * L));
+    const F29<F> want = threadIdx.x == 0 ? f29_reduce<F>(f29_one<F>()) : f29_zero<F>();
+    uint32_t diff = 0;
+    for (int i = 0; i < L; i++) diff |= v.v[i] ^ want.v[i];
+    flag[2 + threadIdx.x] = diff;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t bad = 0;
+    for (int i = 0; i < 12; i++) bad |= flag[2 + i];
+    *ok = (vw_smem[OFF + S::FLAG] == 1u || vw_smem[READY + 1] != 0u) ? 2u : (bad == 0 ? 1u : 0u);
+  }
+}
+
 // Debug / measurement (kzgx_debug_vw_bench, not in kzg_gpu.h): the latency
 // of one wave-wide Fp12 op, iterated `iters` times on arbitrary values < m
 // in LDS: 0 cyclotomic squaring, 1 dense product, 2 squaring, 3 line
@@ -1598,6 +1790,24 @@ static int pair2_wave_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const u
                      qfin, d_ok);
   KZGX_TRY_HIP(hipGetLastError());
   return KZGX_OK;
+}
+
+template <class C>
+static int pair2_fused_impl(const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+                            const uint32_t* d_buf, uint32_t* d_ok, hipStream_t st) {
+  const uint32_t* lines = d_buf + vw_tab_words<C>();
+  const uint32_t* qfin = lines + (size_t)2 * VWave<C>::NL * VWave<C>::LW;
+  hipLaunchKernelGGL(k_pair2_fused<C>, dim3(1), dim3(192), Fused<C>::WORDS * 4, st, d_p, d_p_inf, d_q, d_q_inf, lines,
+                     qfin, d_ok);
+  KZGX_TRY_HIP(hipGetLastError());
+  return KZGX_OK;
+}
+
+int pair2_fused(Ctx* ctx, const uint32_t* d_p, const uint32_t* d_p_inf, const uint32_t* d_q, const uint32_t* d_q_inf,
+                const uint32_t* d_vw, uint32_t* d_ok, hipStream_t st) {
+  ProfScope p(ctx, st, "pair2_fused");
+  return ctx->curve == KZGX_CURVE_BN254 ? pair2_fused_impl<BN254G1>(d_p, d_p_inf, d_q, d_q_inf, d_vw, d_ok, st)
+                                        : pair2_fused_impl<BLS12381G1>(d_p, d_p_inf, d_q, d_q_inf, d_vw, d_ok, st);
 }
 
 size_t pair2_wave_scratch_bytes(int curve) {
