@@ -252,6 +252,33 @@ def test_verify_proof_degenerate_setups(name, C, ctxs):
 
 
 @pytest.mark.parametrize("name,C", CURVES)
+def test_verify_proof_vanishing_at_tau(name, C, ctxs):
+    """an opening set holding tau itself: Z(tau) = 0, so [Z(tau)]G2 is the
+    point at infinity (the fused pairing kernel's Q_0 = O case: no line
+    chain, e(pi, O) = 1) and the check reduces to C == [I(tau)]G1"""
+    ctx = ctxs(name)
+    tau = 2
+    _setup(ctx, C, tau, 12)
+    P = K.random_scalars(C, 10, seed=77)
+    S = scalars(P)
+    com, cinf = ctx.msm(S)
+    xs = [2, 3, 4]
+    pts = K.evaluate_points(C, P, 2, 3)
+    prf, pinf = ctx.prove_range(S, scalars(xs))
+    ys = [y for _, y in pts]
+    exp = K.verify_proof_tau(C, tau, 12, None if cinf else (to_int(com[:w64(C)]), to_int(com[w64(C):])),
+                             None if pinf else (to_int(prf[:w64(C)]), to_int(prf[w64(C):])), pts)
+    assert ctx.verify_proof(com, cinf, prf, pinf, scalars(xs), scalars(ys)) == exp == True  # noqa: E712
+    for k in (0, 2):  # y at tau itself (I(tau) moves), and at another point
+        bad = list(ys)
+        bad[k] = (bad[k] + 1) % C.r
+        bpts = [(x, y) for (x, _), y in zip(pts, bad)]
+        exp = K.verify_proof_tau(C, tau, 12, None if cinf else (to_int(com[:w64(C)]), to_int(com[w64(C):])),
+                                 None if pinf else (to_int(prf[:w64(C)]), to_int(prf[w64(C):])), bpts)
+        assert ctx.verify_proof(com, cinf, prf, pinf, scalars(xs), scalars(bad)) == exp, k
+
+
+@pytest.mark.parametrize("name,C", CURVES)
 @pytest.mark.parametrize("wave_max", [4096, 0], ids=["wave", "lane"])
 def test_verify_single_batch(name, C, ctxs, wave_max):
     """batched single-point verifies == verify_proof(commit, proof, {(z, y)})
