@@ -394,17 +394,24 @@ __global__ __launch_bounds__(64) void k_g2_validate(const uint32_t* __restrict__
 // out = a - b for canonical affine G1 points (the C - [I(tau)]G1 of
 // verify_proof, trusted_setup.cpp:245-247)
 template <class C>
-__global__ void k_g1_sub(const uint32_t* __restrict__ a, const uint32_t* __restrict__ a_inf,
+__global__ __launch_bounds__(64) void k_g1_sub(const uint32_t* __restrict__ a, const uint32_t* __restrict__ a_inf,
                          const uint32_t* __restrict__ b, const uint32_t* __restrict__ b_inf, uint32_t* __restrict__ out,
                          uint32_t* __restrict__ out_inf) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // every lane of the one wave holds the same point: the conversion's
+  // inversion runs wave-uniform (xyzz_to_canonical_lane), lane 0 stores
+  constexpr int N = C::Fp::N;
   Xyzz<C> acc = xyzz_inf<C>();
   Affine<C> pa, pb;
   if (affine_from_canonical<C>(a, pa) && !(a_inf && *a_inf)) acc = xyzz_from_affine<C>(pa);
   if (affine_from_canonical<C>(b, pb) && !(b_inf && *b_inf)) acc = xyzz_add_affine<C>(acc, affine_neg<C>(pb));
-  Affine<C> r;
-  const bool fin = xyzz_to_affine_lane<C>(acc, r);  // thread 0 alone
-  affine_to_canonical<C>(out, r, fin);
+  uint32_t wx[N], wy[N];
+  const bool fin = xyzz_to_canonical_lane<C>(acc, wx, wy);
+  if (threadIdx.x != 0) return;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    out[k] = wx[k];
+    out[N + k] = wy[k];
+  }
   *out_inf = fin ? 0u : 1u;
 }
 
