@@ -202,10 +202,14 @@ def test_reference_multi_proof(name, C, N):
 def cfg5_poly():
     C = K.BN254
     n = (1 << 20) + 1
-    rng = np.random.default_rng(0x4B5A47)
-    S = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
-    S[:, 3] &= np.uint64((1 << 59) - 1)
+    from bench import random_fr
+    # full-range scalars in [0, r) (c = 16's top window filled, as the
+    # 262 145-point BIG cases of test_gpu_pippenger_buckets.py), plus 0,
+    # r - 1 and the top bit alone
+    S = random_fr(np.random.default_rng(0x4B5A47), (n,), C.r)
     S[17] = 0
+    for k, v in ((18, C.r - 1), (19, 1 << 253)):
+        S[k] = [(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)]
     import corc
     ptau = corc.poly_eval("BN254", S, K.default_tau(C))
     return S, g_mul("BN254", C, ptau)
