@@ -37,6 +37,8 @@ def run(srs_n, n):
     ctx = kzgx.Context("BN254")
     try:
         ctx.set_default_table(0)
+        if os.environ.get("KZGX_SEG"):  # A/B: entries per accumulation thread (default 128)
+            ctx.set_segment(int(os.environ["KZGX_SEG"]))
         ctx.gen_srs(tau, srs_n)
         d_s = torch.from_numpy(P[:n].copy().view(np.int64)).cuda()
         d_o = torch.zeros((8,), dtype=torch.int64, device="cuda")
@@ -60,7 +62,7 @@ def run(srs_n, n):
         rec = {"srs_points": srs_n, "n": n, "median_ms": float(np.median(ts)), "min_ms": float(min(ts)),
                "per_s": 1e3 / float(np.median(ts)), "checked": got == exp,
                "path": "chunked c=12" if os.environ.get("KZGX_BIG_MIN") == "0" else "wide-window",
-               "big_window": os.environ.get("KZGX_BIG_WINDOW", "auto")}
+               "big_window": os.environ.get("KZGX_BIG_WINDOW", "auto"), "seg": os.environ.get("KZGX_SEG", "128")}
         print(json.dumps(rec), flush=True)
         assert got == exp
     finally:
