@@ -318,8 +318,15 @@ def main():
         "",
     ]
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "curve_consts.h")
+    text = "\n".join(out)
+    # unchanged constants leave the header (and its mtime) alone: every object
+    # includes it, so a rewrite would make build() recompile everything
+    if os.path.exists(path):
+        with open(path) as f:
+            if f.read() == text:
+                return
     with open(path, "w") as f:
-        f.write("\n".join(out))
+        f.write(text)
 
 
 if __name__ == "__main__":
