@@ -53,6 +53,11 @@ struct kzgx_ctx {
   uint8_t* h_pin = nullptr;
   uint8_t* d_pin = nullptr;  // device address of h_pin
   size_t pin_b = 0;
+
+  // verify_proof's side stream (from the device pool, on first use): the G2
+  // half ([Z(tau)]G2) runs there beside the G1 half (I, [I(tau)]G1, C - it)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace kzgx {
@@ -489,7 +494,7 @@ int kzgx_init_device(int curve, int device) {
   KZGX_TRY_HIP(hipSetDevice(device));
   // the streams of the first contexts (kzg::init's default context, the
   // first trusted_setup), created here, outside the timed regions
-  hipStream_t spare[2] = {nullptr, nullptr};
+  hipStream_t spare[3] = {nullptr, nullptr, nullptr};  // (+1: verify_proof's side stream)
   for (auto& s2 : spare) KZGX_TRY_HIP(stream_take(device, &s2));
   for (auto s2 : spare) stream_give(device, s2);
   hipStream_t st = nullptr;
@@ -583,6 +588,12 @@ void kzgx_destroy(kzgx_ctx* ctx) {
   }
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (c.small_ev) (void)hipEventDestroy(c.small_ev);
+  if (ctx->side) {
+    (void)hipStreamSynchronize(ctx->side);
+    stream_give(c.device, ctx->side);
+  }
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   (void)hipStreamSynchronize(c.stream);
   stream_give(c.device, c.stream);
   kzgx::ctx_live_add(c.device, -1);
@@ -1266,6 +1277,13 @@ int vw_ensure(kzgx_ctx* ctx, hipStream_t st) {
   return KZGX_OK;
 }
 
+int side_ready(kzgx_ctx* ctx) {
+  if (!ctx->side) KZGX_TRY_HIP(stream_take(ctx->c.device, &ctx->side));
+  if (!ctx->ev_fork) KZGX_TRY_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+  if (!ctx->ev_join) KZGX_TRY_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  return KZGX_OK;
+}
+
 // KZGX_PAIR2_SPLIT=1: the multi-point verify's pairing as round 6's two
 // launches (k_vlines_wave, then k_pair2_wave) instead of k_pair2_fused (A/B)
 bool split_pair2() {
@@ -1426,19 +1444,38 @@ int kzgx_verify_proof(kzgx_ctx* ctx, const uint64_t* commit_xy, int commit_inf, 
   KZGX_TRY_HIP(hipMemcpyAsync(g1, proof_xy, p1, hipMemcpyHostToDevice, st));
   KZGX_TRY_HIP(hipMemcpyAsync((char*)g1 + 2 * p1, commit_xy, p1, hipMemcpyHostToDevice, st));
   KZGX_TRY_HIP(hipMemcpyAsync(fl, hf, sizeof(hf), hipMemcpyHostToDevice, st));
-  // I and Z (linear_roots_and_polyfit, util.cpp:172-178)
-  KZGX_TRY(kzgx::poly_interpolate(&ctx->c, (const uint32_t*)(b + o_x), (const uint32_t*)(b + o_y), n,
-                                  (uint32_t*)(b + o_I), st));
+  // Z and I (linear_roots_and_polyfit, util.cpp:172-178): Z first, then the
+  // G2 half (p1 = [Z(tau)]G2, ~0.9 ms of lone-lane G2 chains) forks onto the
+  // side stream while this stream takes the G1 half (I, [I(tau)]G1, C - it)
   KZGX_TRY(kzgx::poly_vanishing(&ctx->c, (const uint32_t*)(b + o_x), n, (uint32_t*)(b + o_Z), st));
-  // p2 = C - [I(tau)]G1
-  KZGX_TRY(kzgx::msm_batch(&ctx->c, (const uint32_t*)(b + o_I), n, 1, n * 8, (uint32_t*)((char*)g1 + 3 * p1), fl + 5,
-                           st));
-  KZGX_TRY(kzgx::g1_sub(&ctx->c, (const uint32_t*)((char*)g1 + 2 * p1), fl + 4, (const uint32_t*)((char*)g1 + 3 * p1),
-                        fl + 5, (uint32_t*)((char*)g1 + p1), fl + 1, st));
-  // p1 = [Z(tau)]G2, second pairing's G2 input = G2[0]
+  KZGX_TRY(side_ready(ctx));
+  hipStream_t sd = ctx->side;
+  KZGX_TRY_HIP(hipEventRecord(ctx->ev_fork, st));
+  KZGX_TRY_HIP(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
   uint32_t* g2 = (uint32_t*)(b + o_g2);
-  KZGX_TRY(
-      kzgx::msm_g2(&ctx->c, (const uint32_t*)(b + o_Z), ctx->d_srs2_canon, n + 1, g2, fl + 2, st, g2_table(ctx, n + 1, st)));
+  const int rg2 =
+      kzgx::msm_g2(&ctx->c, (const uint32_t*)(b + o_Z), ctx->d_srs2_canon, n + 1, g2, fl + 2, sd, g2_table(ctx, n + 1, sd));
+  // (joined before any return below: the side work writes into this call's staging)
+  const hipError_t jr = hipEventRecord(ctx->ev_join, sd);
+  auto join = [&]() { return hipStreamWaitEvent(st, ctx->ev_join, 0); };
+  if (rg2 != KZGX_OK || jr != hipSuccess) {
+    (void)hipStreamSynchronize(sd);
+    return rg2 != KZGX_OK ? rg2 : kzgx::hip_fail(jr);
+  }
+  int rg1 = kzgx::poly_interpolate(&ctx->c, (const uint32_t*)(b + o_x), (const uint32_t*)(b + o_y), n,
+                                   (uint32_t*)(b + o_I), st);
+  // p2 = C - [I(tau)]G1
+  if (rg1 == KZGX_OK)
+    rg1 = kzgx::msm_batch(&ctx->c, (const uint32_t*)(b + o_I), n, 1, n * 8, (uint32_t*)((char*)g1 + 3 * p1), fl + 5, st);
+  if (rg1 == KZGX_OK)
+    rg1 = kzgx::g1_sub(&ctx->c, (const uint32_t*)((char*)g1 + 2 * p1), fl + 4, (const uint32_t*)((char*)g1 + 3 * p1),
+                       fl + 5, (uint32_t*)((char*)g1 + p1), fl + 1, st);
+  KZGX_TRY_HIP(join());
+  if (rg1 != KZGX_OK) {
+    (void)hipStreamSynchronize(st);
+    return rg1;
+  }
+  // the second pairing's G2 input = G2[0] (the two-launch path reads it here)
   KZGX_TRY_HIP(hipMemcpyAsync((char*)g2 + p2, ctx->d_srs2_canon, p2, hipMemcpyDeviceToDevice, st));
   // e(proof, p1) == e(p2, G2[0])  <=>  e(proof, p1) e(-p2, G2[0]) == 1 (one wave, one final
   // exponentiation; the booleans of the reference's FP12_equals)
